@@ -1,0 +1,89 @@
+"""ctypes binding of libisr.so (include/isr.h).
+
+This module only mirrors the C structs and loads the library; it holds no
+compute.  A missing or unloadable library raises immediately: there is no
+fallback path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int32, c_size_t, c_void_p
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libisr.so"
+
+TILE_H = 16  # ISR_TILE_H
+TILE_W = 32  # ISR_TILE_W
+
+
+class IsrView(ctypes.Structure):
+    _fields_ = [("data", c_void_p), ("hp", c_int32), ("wp", c_int32), ("cs", c_int32),
+                ("pad", c_int32), ("coff", c_int32)]
+
+
+class IsrConvDesc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
+                ("cin", c_int32), ("cout", c_int32),
+                ("x", IsrView), ("y", IsrView), ("y2", IsrView), ("r1", IsrView), ("r2", IsrView),
+                ("wpack", c_void_p), ("bias", c_void_p),
+                ("slope", c_float), ("s1", c_float), ("s2", c_float), ("shuffle", c_int32)]
+
+
+class IsrHeadDesc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
+                ("cout", c_int32), ("x", c_void_p), ("x_u8", c_int32),
+                ("mean", c_float * 3), ("inv_std", c_float * 3),
+                ("y", IsrView), ("y2", IsrView), ("wpack", c_void_p), ("bias", c_void_p), ("slope", c_float)]
+
+
+class IsrTailDesc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
+                ("cin", c_int32), ("x", IsrView), ("wpack", c_void_p), ("bias", c_void_p),
+                ("y", c_void_p), ("y_u8", c_int32)]
+
+
+# Every symbol include/isr.h declares, with its ctypes signature.
+SIGNATURES = {
+    "isr_conv3x3_packed_bytes": (c_size_t, [c_int32, c_int32]),
+    "isr_pack_conv3x3": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "isr_head9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),
+    "isr_pack_head9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "isr_tail9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),
+    "isr_pack_tail9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "isr_conv3x3_fwd": (c_int32, [POINTER(IsrConvDesc), c_void_p]),
+    "isr_head9x9_fwd": (c_int32, [POINTER(IsrHeadDesc), c_void_p]),
+    "isr_tail9x9_fwd": (c_int32, [POINTER(IsrTailDesc), c_void_p]),
+    "isr_last_error": (ctypes.c_char_p, []),
+    "isr_version": (c_int32, []),
+}
+
+_lib = None
+
+
+class IsrError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libisr.so (built by image_super_resolution_amd._build / __graft_entry__.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = Path(os.environ.get("ISR_LIB", LIB_PATH))
+    if not path.exists():
+        raise IsrError(f"libisr.so not found at {path}; run `python -m image_super_resolution_amd._build` "
+                       "(or __graft_entry__.build()) first — there is no non-HIP fallback")
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().isr_last_error().decode(errors="replace")
+        raise IsrError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,143 @@
+// extern "C" entry points of libisr.so (declared in include/isr.h).
+// Validation happens here so that a bad descriptor never reaches a kernel:
+// every kernel indexes its tiles without bounds checks.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "isr_common.h"
+
+namespace isr {
+int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s);
+int conv3x3_cout_tile(int cout);
+size_t conv3x3_packed_bytes(int cout, int cin);
+int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
+int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s);
+int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s);
+size_t head9x9_packed_bytes(int cout);
+size_t tail9x9_packed_bytes();
+int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
+int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
+}  // namespace isr
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+static int launched(int rc, const char* what) {
+    if (rc != 0) {
+        hipError_t e = hipGetLastError();
+        return fail(ISR_ERR_LAUNCH, "%s: launch failed: %s", what, hipGetErrorString(e));
+    }
+    g_err[0] = 0;
+    return ISR_OK;
+}
+
+// A view must hold rows [-halo, ha + halo) and cols [-halo, wa + halo) of the
+// computed region plus `ch` channels from coff.
+static bool view_ok(const isr_view& v, int ha, int wa, int halo, int ch, const char* name, int align16) {
+    if (!v.data) { fail(ISR_ERR_BAD_DESC, "%s: null data", name); return false; }
+    if (v.pad < halo) { fail(ISR_ERR_BAD_DESC, "%s: pad %d < required halo %d", name, v.pad, halo); return false; }
+    if (v.hp < ha + 2 * v.pad || v.wp < wa + 2 * v.pad) {
+        fail(ISR_ERR_BAD_DESC, "%s: buffer %dx%d (pad %d) smaller than computed region %dx%d", name, v.hp, v.wp, v.pad, ha, wa);
+        return false;
+    }
+    if (v.coff < 0 || v.coff + ch > v.cs) {
+        fail(ISR_ERR_BAD_DESC, "%s: channels [%d,%d) exceed stride %d", name, v.coff, v.coff + ch, v.cs);
+        return false;
+    }
+    if (align16 && ((v.cs % 8) || (v.coff % 8) || ((uintptr_t)v.data % 16))) {
+        fail(ISR_ERR_BAD_DESC, "%s: channel stride/offset must be multiples of 8 and data 16-byte aligned", name);
+        return false;
+    }
+    return true;
+}
+
+extern "C" {
+
+const char* isr_last_error(void) { return g_err; }
+int isr_version(void) { return 1; }
+
+size_t isr_conv3x3_packed_bytes(int32_t cout, int32_t cin) { return isr::conv3x3_packed_bytes(cout, cin); }
+size_t isr_head9x9_packed_bytes(int32_t cout, int32_t cin) { (void)cin; return isr::head9x9_packed_bytes(cout); }
+size_t isr_tail9x9_packed_bytes(int32_t cout, int32_t cin) { (void)cout; (void)cin; return isr::tail9x9_packed_bytes(); }
+
+int isr_pack_conv3x3(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+    if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_conv3x3: null pointer");
+    if (cin <= 0 || cin % 32) return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cin %d must be a positive multiple of 32", cin);
+    if (!(cout == 32 || (cout > 0 && cout % 64 == 0)))
+        return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cout %d must be 32 or a multiple of 64", cout);
+    return launched(isr::conv3x3_pack(w, packed, cout, cin, (hipStream_t)s), "pack_conv3x3");
+}
+
+int isr_pack_head9x9(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+    if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_head9x9: null pointer");
+    if (cout != 64 || cin < 1 || cin > 3) return fail(ISR_ERR_UNSUPPORTED, "pack_head9x9: need cout 64, cin <= 3 (got %d, %d)", cout, cin);
+    return launched(isr::head9x9_pack(w, packed, cout, cin, (hipStream_t)s), "pack_head9x9");
+}
+
+int isr_pack_tail9x9(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+    if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_tail9x9: null pointer");
+    if (cout != 3 || cin != 64) return fail(ISR_ERR_UNSUPPORTED, "pack_tail9x9: need cout 3, cin 64 (got %d, %d)", cout, cin);
+    return launched(isr::tail9x9_pack(w, packed, cout, cin, (hipStream_t)s), "pack_tail9x9");
+}
+
+int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "conv3x3: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0) return fail(ISR_ERR_BAD_DESC, "conv3x3: empty problem n=%d h=%d w=%d", d->n, d->h, d->w);
+    if (d->ha % ISR_TILE_H || d->wa % ISR_TILE_W || d->ha < d->h || d->wa < d->w)
+        return fail(ISR_ERR_BAD_DESC, "conv3x3: computed region %dx%d must cover %dx%d and be a multiple of %dx%d", d->ha, d->wa,
+                    d->h, d->w, ISR_TILE_H, ISR_TILE_W);
+    if (d->cin <= 0 || d->cin % 32) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cin %d must be a multiple of 32", d->cin);
+    if (!(d->cout == 32 || (d->cout > 0 && d->cout % 64 == 0)))
+        return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cout %d must be 32 or a multiple of 64", d->cout);
+    if (!d->wpack) return fail(ISR_ERR_BAD_DESC, "conv3x3: null weights");
+    if (d->shuffle != 1 && d->shuffle != 2) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: shuffle must be 1 or 2");
+    if (!view_ok(d->x, d->ha, d->wa, 1, d->cin, "conv3x3.x", 1)) return ISR_ERR_BAD_DESC;
+    if (d->shuffle == 2) {
+        if (d->cout % 64) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: pixel shuffle needs cout %% 64 == 0");
+        if (d->r1.data || d->r2.data || d->y2.data)
+            return fail(ISR_ERR_UNSUPPORTED, "conv3x3: pixel shuffle store takes no residual / second output");
+        if (!view_ok(d->y, 2 * d->ha, 2 * d->wa, 0, d->cout / 4, "conv3x3.y", 1)) return ISR_ERR_BAD_DESC;
+    } else {
+        if (!view_ok(d->y, d->ha, d->wa, 0, d->cout, "conv3x3.y", 1)) return ISR_ERR_BAD_DESC;
+        if (d->y2.data && !view_ok(d->y2, d->ha, d->wa, 0, d->cout, "conv3x3.y2", 1)) return ISR_ERR_BAD_DESC;
+        if (d->r1.data && !view_ok(d->r1, d->ha, d->wa, 0, d->cout, "conv3x3.r1", 1)) return ISR_ERR_BAD_DESC;
+        if (d->r2.data && !view_ok(d->r2, d->ha, d->wa, 0, d->cout, "conv3x3.r2", 1)) return ISR_ERR_BAD_DESC;
+    }
+    if (d->bias && ((uintptr_t)d->bias % 16)) return fail(ISR_ERR_BAD_DESC, "conv3x3: bias must be 16-byte aligned");
+    return launched(isr::conv3x3_fwd_dispatch(d, (hipStream_t)s), "conv3x3");
+}
+
+int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "head9x9: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0) return fail(ISR_ERR_BAD_DESC, "head9x9: empty problem");
+    if (d->ha % ISR_TILE_H || d->wa % ISR_TILE_W || d->ha < d->h || d->wa < d->w)
+        return fail(ISR_ERR_BAD_DESC, "head9x9: bad computed region %dx%d for %dx%d", d->ha, d->wa, d->h, d->w);
+    if (d->cout != 64) return fail(ISR_ERR_UNSUPPORTED, "head9x9: cout must be 64");
+    if (!d->x || !d->wpack) return fail(ISR_ERR_BAD_DESC, "head9x9: null input or weights");
+    if (!view_ok(d->y, d->ha, d->wa, 0, 64, "head9x9.y", 1)) return ISR_ERR_BAD_DESC;
+    if (d->y2.data && !view_ok(d->y2, d->ha, d->wa, 0, 64, "head9x9.y2", 1)) return ISR_ERR_BAD_DESC;
+    if (d->bias && ((uintptr_t)d->bias % 16)) return fail(ISR_ERR_BAD_DESC, "head9x9: bias must be 16-byte aligned");
+    return launched(isr::head9x9_fwd_dispatch(d, (hipStream_t)s), "head9x9");
+}
+
+int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "tail9x9: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0) return fail(ISR_ERR_BAD_DESC, "tail9x9: empty problem");
+    if (d->ha % ISR_TILE_H || d->wa % ISR_TILE_W || d->ha < d->h || d->wa < d->w)
+        return fail(ISR_ERR_BAD_DESC, "tail9x9: bad computed region %dx%d for %dx%d", d->ha, d->wa, d->h, d->w);
+    if (d->cin != 64) return fail(ISR_ERR_UNSUPPORTED, "tail9x9: cin must be 64");
+    if (!d->y || !d->wpack) return fail(ISR_ERR_BAD_DESC, "tail9x9: null output or weights");
+    if (!view_ok(d->x, d->ha, d->wa, 4, 64, "tail9x9.x", 1)) return ISR_ERR_BAD_DESC;
+    return launched(isr::tail9x9_fwd_dispatch(d, (hipStream_t)s), "tail9x9");
+}
+
+}  // extern "C"

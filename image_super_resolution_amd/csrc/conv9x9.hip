@@ -1,0 +1,313 @@
+// 9x9 'same' convolutions at the two ends of the generator, on MFMA.
+//
+// head: ResNet.conv0 / EResNet.conv0 = ConvWithoutBN(3, 64, 9) + LeakyReLU
+//       (utils/models.py:596, :625), with Normalize (utils/datasets.py:65-71)
+//       fused for uint8 input.  K = 9 rows x 12 column taps (9 real) x 4
+//       channels (3 real): a k-step of 16 is 4 consecutive column taps of one
+//       row x 4 channels = 2 adjacent pixels x 8 bytes of the channels-padded
+//       LDS halo, so A fragments are plain 16-byte LDS reads (no im2col).
+// tail: ResNet.conv2 / EResNet.conv2 = ConvWithoutBN(64, 3, 9) + Tanh
+//       (utils/models.py:607, :636), with TanhToArrayImage (:448-451) fused
+//       for uint8 output.  N = 3 is too skinny for MFMA, so the kernel moves
+//       the 9 kernel ROWS into N: stage 1 is a 1x9 conv producing
+//       T[y'][x][(ky,co)] (27 of 32 columns used) for the TH+8 input rows of
+//       the tile; stage 2 sums out[y][x][co] = sum_ky T[y+ky-4][x][(ky,co)] in
+//       LDS and applies bias + tanh (+ uint8 quantisation).
+#include "isr_common.h"
+
+namespace isr {
+
+// ============================== head ======================================
+namespace head {
+constexpr int R = 4, WM = 4, NF = 2, TH = R * WM, TW = 32, CT = NF * 32;
+constexpr int HR = TH + 8, HC = 44; // halo cols: 32 + 8, padded so tap groups 9..11 stay in range
+constexpr int HALO_BYTES = HR * HC * 8;
+constexpr int EPS = CT + 4;
+constexpr int EP_BYTES = WM * R * 32 * EPS * 4;
+constexpr int LDS = EP_BYTES > HALO_BYTES ? EP_BYTES : HALO_BYTES;
+}  // namespace head
+
+// packed head weights: [ky 9][ks 3][n 64][k 16] bf16,
+// k = 8h + e → column tap t = 4ks + 2h + (e>>2), channel c = e & 3 (zero if t>=9 or c>=3).
+__global__ __launch_bounds__(256) void head9x9_kernel(isr_head_desc d) {
+    using namespace head;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int img = blockIdx.z;
+    const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
+    const int wave = wave_id();
+    const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+
+    // ---- halo: rows y0-4 .. y0+TH+3, cols x0-4 .. x0+39, 4 ch bf16 ----
+    const size_t plane = (size_t)d.h * d.w;
+    for (int p = threadIdx.x; p < HR * HC; p += 256) {
+        const int row = p / HC, col = p - row * HC;
+        const int yy = y0 - 4 + row, xx = x0 - 4 + col;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (yy >= 0 && yy < d.h && xx >= 0 && xx < d.w && col < 40) {
+            const size_t o = (size_t)img * 3 * plane + (size_t)yy * d.w + xx;
+            if (d.x_u8) {
+                const uint8_t* xp = (const uint8_t*)d.x;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) v[c] = ((float)xp[o + c * plane] / 255.f - d.mean[c]) * d.inv_std[c];
+            } else {
+                const float* xp = (const float*)d.x;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) v[c] = xp[o + c * plane];
+            }
+        }
+        bf16x4 t;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[c] = (__bf16)v[c];
+        *reinterpret_cast<bf16x4*>(smem + p * 8) = t;
+    }
+    __syncthreads();
+
+    f32x16 acc[R][NF];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) acc[r][f][g] = 0.f;
+
+    const char* wp = (const char*)d.wpack;
+#pragma unroll 1
+    for (int ks = 0; ks < 3; ++ks) {
+        bf16x8 b[9][NF];
+#pragma unroll
+        for (int ky = 0; ky < 9; ++ky)
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                b[ky][f] = *reinterpret_cast<const bf16x8*>(wp + (((ky * 3 + ks) * CT + f * 32 + l31) * 16 + hh * 8) * 2);
+#pragma unroll
+        for (int i = 0; i < R + 8; ++i) {
+            const char* ap = smem + ((wave * R + i) * HC + l31 + 4 * ks + 2 * hh) * 8;
+            bf16x4 lo = *reinterpret_cast<const bf16x4*>(ap);
+            bf16x4 hi = *reinterpret_cast<const bf16x4*>(ap + 8);
+            bf16x8 a;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { a[e] = lo[e]; a[4 + e] = hi[e]; }
+#pragma unroll
+            for (int ky = 0; ky < 9; ++ky) {
+                const int r = i - ky;
+                if (r >= 0 && r < R) {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) acc[r][f] = mfma32(a, b[ky][f], acc[r][f]);
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    float* ep = reinterpret_cast<float*>(smem) + wave * (R * 32 * EPS);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int px = (g & 3) + 8 * (g >> 2) + 4 * hh;
+                ep[(r * 32 + px) * EPS + f * 32 + l31] = acc[r][f][g];
+            }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+
+    Epi e;
+    e.bias = d.bias; e.slope = d.slope; e.s1 = 1.f; e.s2 = 1.f;
+    e.y = d.y; e.y2 = d.y2; e.r1.data = nullptr; e.r2.data = nullptr; e.h = d.h; e.w = d.w;
+    constexpr int CG = CT / 8;
+#pragma unroll 4
+    for (int it = 0; it < R * CT / 16; ++it) {
+        const int jj = lane + 64 * it;
+        const int cg = jj % CG, p = jj / CG;
+        const int r = p >> 5, px = p & 31;
+        float v[8];
+        const float* src = ep + (r * 32 + px) * EPS + cg * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = src[k];
+        epi_plain8(e, v, img, y0 + wave * R + r, x0 + px, cg * 8);
+    }
+}
+
+__global__ void pack_head_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
+    const int total = 9 * 3 * cout * 16;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        int rem = idx;
+        const int k = rem % 16; rem /= 16;
+        const int n = rem % cout; rem /= cout;
+        const int ks = rem % 3; rem /= 3;
+        const int ky = rem;
+        const int hh = k >> 3, e = k & 7;
+        const int t = 4 * ks + 2 * hh + (e >> 2), c = e & 3;
+        float v = 0.f;
+        if (t < 9 && c < cin) v = w[(((size_t)n * cin + c) * 9 + ky) * 9 + t];
+        out[idx] = (__bf16)v;
+    }
+}
+
+// ============================== tail ======================================
+namespace tail {
+constexpr int TH = 16, TW = 32, WM = 4;
+constexpr int TR = TH + 8;        // T rows (input rows of the tile)
+constexpr int RT = TR / WM;       // T rows per wave (6)
+constexpr int HC = TW + 8;        // 40 halo cols
+constexpr int HALO_UNITS = TR * HC * 4;       // 3840
+constexpr int HALO_INSTR = HALO_UNITS / 64;   // 60
+constexpr int HALO_BYTES = HALO_UNITS * 16;   // 61440
+constexpr int W_BYTES = 9 * 2 * 2 * 32 * 32;  // [kx][chunk][ks][n][hpos][8] bf16 = 36864
+constexpr int W_INSTR = W_BYTES / 1024;       // 36
+constexpr int TS = 33;                        // floats per pixel in the T image (conflict-free column sums)
+constexpr int T_BYTES = TR * 32 * TS * 4;     // 101376
+constexpr int P1 = HALO_BYTES + W_BYTES;      // 98304
+constexpr int LDS = P1 > T_BYTES ? P1 : T_BYTES;
+static_assert(HALO_UNITS % 64 == 0, "");
+}  // namespace tail
+
+// packed tail weights: [kx 9][chunk 2][ks 2][n 32][hpos 2][8] bf16,
+// n = ky*3 + co (27 used), element = W[co][chunk*32 + ks*16 + h*8 + e][ky][kx], h = hpos ^ ((n>>3)&1).
+__global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
+    using namespace tail;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int img = blockIdx.z;
+    const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
+    const int wave = wave_id();
+    const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+
+    const char* xbase = view_px(d.x, img, y0 - 4, x0 - 4);
+    const int xrow = d.x.wp * d.x.cs * 2, xpix = d.x.cs * 2;
+    char* halo = smem;
+    char* wl = smem + HALO_BYTES;
+
+    f32x16 acc[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
+
+#pragma unroll 1
+    for (int chunk = 0; chunk < 2; ++chunk) {
+        if (chunk == 0) {
+            for (int j = wave; j < W_INSTR; j += WM)
+                glds16((const char*)d.wpack + j * 1024 + lane * 16, wl + j * 1024);
+        }
+        for (int j = wave; j < HALO_INSTR; j += WM) {
+            const int u = j * 64 + lane;
+            const int q = u >> 2, cpos = u & 3;
+            const int row = q / HC, col = q - row * HC;
+            const int c = cpos ^ ((q >> 2) & 3);
+            glds16(xbase + row * xrow + col * xpix + chunk * 64 + c * 16, halo + j * 1024);
+        }
+        wait_vm0();
+        __syncthreads();
+#pragma unroll
+        for (int kx = 0; kx < 9; ++kx) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int n = l31;
+                const bf16x8 b = lds_read16(wl + ((((kx * 2 + chunk) * 2 + ks) * 32 + n) * 2 + (hh ^ ((n >> 3) & 1))) * 16);
+                const int c = 2 * ks + hh;
+#pragma unroll
+                for (int t = 0; t < RT; ++t) {
+                    const int q = (wave * RT + t) * HC + kx + l31;
+                    acc[t] = mfma32(lds_read16(halo + halo_unit(q, c) * 16), b, acc[t]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    float* T = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int px = (g & 3) + 8 * (g >> 2) + 4 * hh;
+            T[((wave * RT + t) * 32 + px) * TS + l31] = acc[t][g];
+        }
+    __syncthreads();
+
+    const size_t plane = (size_t)d.h * d.w;
+    for (int item = threadIdx.x; item < TH * TW; item += 256) {
+        const int yr = item >> 5, px = item & 31;
+        const int yy = y0 + yr, xx = x0 + px;
+        float s[3];
+#pragma unroll
+        for (int co = 0; co < 3; ++co) s[co] = d.bias ? d.bias[co] : 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 9; ++ky) {
+            const float* tp = T + ((yr + ky) * 32 + px) * TS + ky * 3;
+#pragma unroll
+            for (int co = 0; co < 3; ++co) s[co] += tp[co];
+        }
+        if (yy < d.h && xx < d.w) {
+            const size_t o = (size_t)img * 3 * plane + (size_t)yy * d.w + xx;
+#pragma unroll
+            for (int co = 0; co < 3; ++co) {
+                const float t = tanhf(s[co]);
+                if (d.y_u8) {
+                    const float q = rintf((t + 1.f) / 2.f * 255.f);
+                    ((uint8_t*)d.y)[o + co * plane] = (uint8_t)fminf(fmaxf(q, 0.f), 255.f);
+                } else {
+                    ((float*)d.y)[o + co * plane] = t;
+                }
+            }
+        }
+    }
+}
+
+__global__ void pack_tail_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
+    const int total = tail::W_BYTES / 2;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        int rem = idx;
+        const int e = rem % 8; rem /= 8;
+        const int hpos = rem % 2; rem /= 2;
+        const int n = rem % 32; rem /= 32;
+        const int ks = rem % 2; rem /= 2;
+        const int chunk = rem % 2; rem /= 2;
+        const int kx = rem;
+        const int hh = hpos ^ ((n >> 3) & 1);
+        const int ky = n / 3, co = n % 3;
+        const int ci = chunk * 32 + ks * 16 + hh * 8 + e;
+        float v = 0.f;
+        if (n < 27 && co < cout) v = w[(((size_t)co * cin + ci) * 9 + ky) * 9 + kx];
+        out[idx] = (__bf16)v;
+    }
+}
+
+// ============================== launchers ================================
+int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)head9x9_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, head::LDS);
+        attr = true;
+    }
+    dim3 grid(d->wa / head::TW, d->ha / head::TH, d->n);
+    hipLaunchKernelGGL(head9x9_kernel, grid, dim3(256), head::LDS, s, *d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)tail9x9_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, tail::LDS);
+        attr = true;
+    }
+    dim3 grid(d->wa / tail::TW, d->ha / tail::TH, d->n);
+    hipLaunchKernelGGL(tail9x9_kernel, grid, dim3(256), tail::LDS, s, *d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t head9x9_packed_bytes(int cout) { return (size_t)9 * 3 * cout * 16 * 2; }
+size_t tail9x9_packed_bytes() { return tail::W_BYTES; }
+
+int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s) {
+    hipLaunchKernelGGL(pack_head_kernel, dim3(64), dim3(256), 0, s, w, (__bf16*)out, cout, cin);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s) {
+    hipLaunchKernelGGL(pack_tail_kernel, dim3(64), dim3(256), 0, s, w, (__bf16*)out, cout, cin);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace isr

@@ -1,0 +1,103 @@
+// Shared device helpers for libisr (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "isr.h"
+
+namespace isr {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+#define ISR_LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+// One 32x32x16 bf16 MFMA: acc += A(32x16) * B(16x32).
+// Lane l (r = l & 31, h = l >> 5) supplies A[r][8h..8h+7] and B[8h..8h+7][r];
+// accumulator register g of lane l holds D[(g&3) + 8*(g>>2) + 4*h][r].
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 acc) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 lds_read16(const char* p) {
+    return *reinterpret_cast<const bf16x8*>(p);
+}
+
+// Asynchronous 16-byte-per-lane global → LDS copy (global_load_lds_dwordx4).
+// The LDS destination is wave-uniform `lds` + lane*16.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds) {
+    __builtin_amdgcn_global_load_lds(gsrc, ISR_LDS_PTR(lds), 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ int wave_id() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+// Byte address of interior pixel (img, y, x), channel 0 of a view.
+__device__ __forceinline__ char* view_px(const isr_view& v, int img, int y, int x) {
+    size_t pix = ((size_t)img * v.hp + (y + v.pad)) * (size_t)v.wp + (size_t)(x + v.pad);
+    return (char*)v.data + (pix * (size_t)v.cs + (size_t)v.coff) * 2;
+}
+
+// Swizzled position of 16-byte unit (pixel q, channel-chunk c in 0..3) in an
+// LDS halo image with 64 B per pixel.  XOR with bits 2..3 of q makes the
+// 32-consecutive-pixel ds_read_b128 of an MFMA A fragment bank-conflict free.
+__device__ __forceinline__ int halo_unit(int q, int c) { return q * 4 + (c ^ ((q >> 2) & 3)); }
+
+__device__ __forceinline__ void load8_bf16(const char* p, float* v) {
+    bf16x8 t = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)t[e];
+}
+
+__device__ __forceinline__ void store8_bf16(char* p, const float* v) {
+    bf16x8 t;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = (__bf16)v[e];
+    *reinterpret_cast<bf16x8*>(p) = t;
+}
+
+// Fused epilogue on 8 consecutive output channels [co, co+8) of one pixel.
+// v = leaky(v + bias); v = v*s1 + r1; v = v*s2 + r2; zero outside the valid region.
+struct Epi {
+    const float* bias;
+    float slope, s1, s2;
+    isr_view y, y2, r1, r2;
+    int h, w;
+};
+
+__device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int yy, int xx, int co) {
+    if (e.bias) {
+        f32x4 b0 = *reinterpret_cast<const f32x4*>(e.bias + co);
+        f32x4 b1 = *reinterpret_cast<const f32x4*>(e.bias + co + 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { v[k] += b0[k]; v[4 + k] += b1[k]; }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] >= 0.f ? v[k] : v[k] * e.slope;
+    const bool valid = (yy < e.h) && (xx < e.w);
+    if (e.r1.data) {
+        float r[8];
+        load8_bf16(view_px(e.r1, img, yy, xx) + co * 2, r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] * e.s1 + r[k];
+    }
+    if (e.r2.data) {
+        float r[8];
+        load8_bf16(view_px(e.r2, img, yy, xx) + co * 2, r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] * e.s2 + r[k];
+    }
+    if (!valid) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = 0.f;
+    }
+    store8_bf16(view_px(e.y, img, yy, xx) + co * 2, v);
+    if (e.y2.data) store8_bf16(view_px(e.y2, img, yy, xx) + co * 2, v);
+}
+
+}  // namespace isr

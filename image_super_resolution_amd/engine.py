@@ -1,0 +1,179 @@
+"""Inference engine for the RRDB generators on libisr (MI355X).
+
+Executes ResNet / EResNet (utils/models.py:592-650) — optionally wrapped as
+the uint8 `Model` (:723-739) — entirely through the HIP kernels:
+
+  head9x9   conv0 (+Normalize for uint8 input)       → feat, X[0:64]
+  16 x RRDB, each 3 x RDB on rotating dense buffers X → Y → Z → X:
+    conv3x3 growth k=0..3  src[0:64+32k] → src[64+32k : 96+32k]     (torch.cat eliminated)
+    conv3x3 final          src[0:192] → dst[0:64],  v*0.2 + src[0:64]
+                           (third RDB: ((v*0.2 + Z) * 0.2 + X) in place = RRDB residual)
+  conv3x3 conv1            X[0:64] → feat (in place), v + feat    (trunk residual)
+  conv3x3 scaler x S       64 → 256, PixelShuffle(2) + LeakyReLU on store
+  tail9x9 conv2 + tanh     → NCHW fp32 (or uint8 = TanhToArrayImage)
+
+Activations are NHWC bf16 with a zero border (ops.ActBuffer); the dense
+buffers keep the 192-channel concat resident so no concat is ever copied.
+BatchNorm is folded into the conv (fuse_conv_and_bn, :366-406) at pack time.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import ops
+from .ops import ActBuffer
+
+LEAKY_DEFAULT = 0.01
+
+
+def _fold(sd: dict, prefix: str, device) -> tuple[torch.Tensor, torch.Tensor]:
+    """(W, b) fp32 of Conv / ConvWithoutBN `prefix`, BN folded as fuse_conv_and_bn does."""
+    w = sd[f"{prefix}.conv.weight"].detach().to(device=device, dtype=torch.float32)
+    b = sd.get(f"{prefix}.conv.bias")
+    b = torch.zeros(w.shape[0], device=device) if b is None else b.detach().to(device=device, dtype=torch.float32)
+    if f"{prefix}.bn.weight" in sd:
+        g = sd[f"{prefix}.bn.weight"].detach().to(device, torch.float32)
+        beta = sd[f"{prefix}.bn.bias"].detach().to(device, torch.float32)
+        mu = sd[f"{prefix}.bn.running_mean"].detach().to(device, torch.float32)
+        var = sd[f"{prefix}.bn.running_var"].detach().to(device, torch.float32)
+        eps = 1e-5
+        s = g / torch.sqrt(eps + var)
+        w = w * s.view(-1, 1, 1, 1)
+        b = s * b + (beta - g * mu / torch.sqrt(var + eps))
+    return w, b.contiguous()
+
+
+@dataclass
+class PackedConv:
+    w: torch.Tensor  # packed bf16
+    b: torch.Tensor  # fp32 bias
+    cin: int
+    cout: int
+
+
+@dataclass
+class GeneratorWeights:
+    head: PackedConv
+    rdb: list[list[list[PackedConv]]]  # [block][rdb 0..2][conv 0..4]
+    conv1: PackedConv
+    scalers: list[PackedConv]
+    tail: PackedConv
+    conv0_slope: float
+    add_rate: float
+    buffers: dict = field(default_factory=dict)
+
+
+def _pack3(sd, prefix, device) -> PackedConv:
+    w, b = _fold(sd, prefix, device)
+    return PackedConv(ops.pack_conv3x3(w), b, w.shape[1], w.shape[0])
+
+
+def count_blocks(sd: dict, prefix: str = "") -> int:
+    p = f"{prefix}residual."
+    return len({int(k[len(p):].split(".")[0]) for k in sd if k.startswith(p)})
+
+
+def count_scalers(sd: dict, prefix: str = "") -> int:
+    p = f"{prefix}scaler."
+    return len({int(k[len(p):].split(".")[0]) for k in sd if k.startswith(p)})
+
+
+def pack_generator(sd: dict, *, enchant: bool, add_rate: float = 0.2, prefix: str = "",
+                   device="cuda") -> GeneratorWeights:
+    """Pack a ResNet/EResNet state_dict (reference key schema, fused or not)."""
+    p = prefix
+    w0, b0 = _fold(sd, f"{p}conv0", device)
+    head = PackedConv(ops.pack_head9x9(w0), b0, w0.shape[1], w0.shape[0])
+    nb = count_blocks(sd, p)
+    rdb = [[[_pack3(sd, f"{p}residual.{i}.net.{r}.{c}", device)
+             for c in ("conv0", "conv1", "conv2", "conv3", "conv")] for r in range(3)] for i in range(nb)]
+    conv1 = _pack3(sd, f"{p}conv1", device)
+    scalers = [_pack3(sd, f"{p}scaler.{s}.net.0", device) for s in range(count_scalers(sd, p))]
+    w2, b2 = _fold(sd, f"{p}conv2", device)
+    tail = PackedConv(ops.pack_tail9x9(w2), b2, w2.shape[1], w2.shape[0])
+    return GeneratorWeights(head, rdb, conv1, scalers, tail, LEAKY_DEFAULT if enchant else 0.2, add_rate)
+
+
+class GeneratorBuffers:
+    """Activation buffers for one input geometry, allocated once and reused."""
+
+    def __init__(self, n: int, h: int, w: int, n_scalers: int, device):
+        self.feat = ActBuffer.alloc(n, h, w, 64, 1, device)
+        self.dense = [ActBuffer.alloc(n, h, w, 192, 1, device) for _ in range(3)]
+        self.up = []
+        hh, ww = h, w
+        ha, wa = self.feat.ha, self.feat.wa
+        for s in range(n_scalers):
+            hh, ww, ha, wa = 2 * hh, 2 * ww, 2 * ha, 2 * wa
+            pad = 4 if s == n_scalers - 1 else 1
+            self.up.append(ActBuffer.alloc(n, hh, ww, 64, pad, device, ha=ha, wa=wa))
+
+
+def rdb_forward(convs: list[PackedConv], src: ActBuffer, dst: ActBuffer, add_rate: float, *,
+                r2: ActBuffer | None = None, s2: float = 1.0, slope: float = LEAKY_DEFAULT) -> None:
+    """RDB.forward (utils/models.py:265-271) on a 192-channel dense buffer.
+
+    src[0:64] holds the block input; growth conv k appends channels
+    [64+32k, 96+32k) in place (the torch.cat chain), the final conv writes
+    dst[0:64] = conv*add_rate + src[0:64] (then *s2 + r2 when r2 is given —
+    the enclosing RRDB's residual, utils/models.py:317)."""
+    for k in range(4):
+        pc = convs[k]
+        ops.conv3x3(src, pc.cin, pc.w, pc.b, pc.cout, src, y_coff=pc.cin, slope=slope)
+    pc = convs[4]
+    ops.conv3x3(src, pc.cin, pc.w, pc.b, pc.cout, dst, slope=1.0, r1=src, s1=add_rate, r2=r2, s2=s2)
+
+
+def rrdb_forward(blk, X: ActBuffer, Y: ActBuffer, Z: ActBuffer, add_rate: float, *,
+                 slope: float = LEAKY_DEFAULT) -> None:
+    """RRDB.forward (utils/models.py:316-317): X → Y → Z → X[0:64] (in place), where
+    the last RDB's epilogue adds the RRDB residual X[0:64] at the same pixel."""
+    rdb_forward(blk[0], X, Y, add_rate, slope=slope)
+    rdb_forward(blk[1], Y, Z, add_rate, slope=slope)
+    rdb_forward(blk[2], Z, X, add_rate, r2=X, s2=add_rate, slope=slope)
+
+
+def run_generator(gw: GeneratorWeights, x: torch.Tensor, *, out_u8: bool = False,
+                  mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)) -> torch.Tensor:
+    """x: NCHW [n,3,h,w] fp32 (normalised) or uint8 (Normalize fused) on the GPU."""
+    n, c, h, w = x.shape
+    if c != 3:
+        raise ValueError(f"generator expects 3 input channels, got {c}")
+    key = (n, h, w, x.device)
+    bufs = gw.buffers.get(key)
+    if bufs is None:
+        bufs = GeneratorBuffers(n, h, w, len(gw.scalers), x.device)
+        gw.buffers = {key: bufs}  # keep one geometry resident
+    feat = bufs.feat
+    X, Y, Z = bufs.dense
+    ar = gw.add_rate
+    ops.head9x9(x, gw.head.w, gw.head.b, feat, slope=gw.conv0_slope, y2=X, mean=mean, std=std)
+    for blk in gw.rdb:
+        rrdb_forward(blk, X, Y, Z, ar)
+    pc = gw.conv1
+    ops.conv3x3(X, pc.cin, pc.w, pc.b, pc.cout, feat, slope=1.0, r1=feat, s1=1.0)
+    cur = feat
+    for s, pc in enumerate(gw.scalers):
+        nxt = bufs.up[s]
+        ops.conv3x3(cur, pc.cin, pc.w, pc.b, pc.cout, nxt, slope=LEAKY_DEFAULT, shuffle=2)
+        cur = nxt
+    out = torch.empty((n, 3, cur.h, cur.w), dtype=torch.uint8 if out_u8 else torch.float32, device=x.device)
+    ops.tail9x9(cur, gw.tail.w, gw.tail.b, out)
+    return out
+
+
+def generator_flops(h: int, w: int, num_blocks: int = 16, n_scalers: int = 2) -> float:
+    """Algorithmic FLOPs (2*MAC) of one generator forward on an h x w LR image."""
+    px = h * w
+    macs = px * 64 * 3 * 81  # conv0
+    rdb = sum((64 + 32 * k) * 32 * 9 for k in range(4)) + 192 * 64 * 9
+    macs += px * num_blocks * 3 * rdb
+    macs += px * 64 * 64 * 9  # conv1
+    p = px
+    for _ in range(n_scalers):
+        macs += p * 64 * 256 * 9
+        p *= 4
+    macs += p * 64 * 3 * 81  # conv2
+    return 2.0 * macs

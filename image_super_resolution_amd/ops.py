@@ -1,0 +1,177 @@
+"""Thin host wrappers over the libisr C-ABI.
+
+PyTorch is plumbing here: it allocates device memory and supplies the current
+HIP stream; every byte of compute happens in libisr.so.  All functions require
+CUDA (HIP) tensors and raise otherwise.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import IsrConvDesc, IsrHeadDesc, IsrTailDesc, IsrView, TILE_H, TILE_W, check
+
+
+def round_up(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+def _stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _require_gpu(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"{what}: image_super_resolution_amd runs on the MI355X HIP path only "
+                           f"(got a {t.device} tensor); the CPU restatement lives in oracle/ for tests")
+
+
+@dataclass
+class ActBuffer:
+    """NHWC bf16 activation buffer [n][ha+2p][wa+2p][c] with a zero border of p pixels.
+
+    (h, w) is the valid image size, (ha, wa) the tile-aligned computed extent.
+    Kernels keep every position outside (h, w) at exactly zero, so the border
+    and alignment slack act as the convolution's zero padding.
+    """
+    t: torch.Tensor
+    n: int
+    h: int
+    w: int
+    ha: int
+    wa: int
+    pad: int
+
+    @staticmethod
+    def alloc(n: int, h: int, w: int, c: int, pad: int, device, ha: int | None = None,
+              wa: int | None = None) -> "ActBuffer":
+        ha = round_up(h, TILE_H) if ha is None else ha
+        wa = round_up(w, TILE_W) if wa is None else wa
+        t = torch.zeros((n, ha + 2 * pad, wa + 2 * pad, c), dtype=torch.bfloat16, device=device)
+        return ActBuffer(t, n, h, w, ha, wa, pad)
+
+    @property
+    def c(self) -> int:
+        return self.t.shape[3]
+
+    def view(self, coff: int = 0) -> IsrView:
+        return IsrView(self.t.data_ptr(), self.t.shape[1], self.t.shape[2], self.t.shape[3], self.pad, coff)
+
+    def interior(self, c0: int = 0, c1: int | None = None) -> torch.Tensor:
+        """Valid region as a [n, h, w, c] view (for tests / debugging)."""
+        p = self.pad
+        return self.t[:, p:p + self.h, p:p + self.w, c0:c1]
+
+    @staticmethod
+    def from_nchw(x: torch.Tensor, pad: int = 1, c_alloc: int | None = None) -> "ActBuffer":
+        n, c, h, w = x.shape
+        buf = ActBuffer.alloc(n, h, w, c_alloc or c, pad, x.device)
+        buf.t[:, pad:pad + h, pad:pad + w, :c] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+        return buf
+
+    def to_nchw(self, c0: int = 0, c1: int | None = None) -> torch.Tensor:
+        return self.interior(c0, c1).permute(0, 3, 1, 2).float()
+
+
+_NULL_VIEW = IsrView(None, 0, 0, 0, 0, 0)
+
+
+# ---------------------------------------------------------------- packing
+def pack_conv3x3(w: torch.Tensor) -> torch.Tensor:
+    """fp32 OIHW [cout, cin, 3, 3] device weights → packed bf16 kernel layout."""
+    _require_gpu(w, "pack_conv3x3")
+    lib = _lib.load()
+    cout, cin = w.shape[:2]
+    w = w.detach().float().contiguous()
+    out = torch.empty(lib.isr_conv3x3_packed_bytes(cout, cin) // 2, dtype=torch.bfloat16, device=w.device)
+    check(lib.isr_pack_conv3x3(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_conv3x3")
+    return out
+
+
+def pack_head9x9(w: torch.Tensor) -> torch.Tensor:
+    _require_gpu(w, "pack_head9x9")
+    lib = _lib.load()
+    cout, cin = w.shape[:2]
+    w = w.detach().float().contiguous()
+    out = torch.empty(lib.isr_head9x9_packed_bytes(cout, cin) // 2, dtype=torch.bfloat16, device=w.device)
+    check(lib.isr_pack_head9x9(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_head9x9")
+    return out
+
+
+def pack_tail9x9(w: torch.Tensor) -> torch.Tensor:
+    _require_gpu(w, "pack_tail9x9")
+    lib = _lib.load()
+    cout, cin = w.shape[:2]
+    w = w.detach().float().contiguous()
+    out = torch.empty(lib.isr_tail9x9_packed_bytes(cout, cin) // 2, dtype=torch.bfloat16, device=w.device)
+    check(lib.isr_pack_tail9x9(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_tail9x9")
+    return out
+
+
+# ---------------------------------------------------------------- launches
+def conv3x3(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor | None, cout: int,
+            y: ActBuffer, *, x_coff: int = 0, y_coff: int = 0, slope: float = 1.0,
+            r1: ActBuffer | None = None, r1_coff: int = 0, s1: float = 1.0,
+            r2: ActBuffer | None = None, r2_coff: int = 0, s2: float = 1.0,
+            y2: ActBuffer | None = None, y2_coff: int = 0, shuffle: int = 1) -> None:
+    """y[..., y_coff:y_coff+cout] = epilogue(conv3x3(x[..., x_coff:x_coff+cin]))."""
+    d = IsrConvDesc()
+    d.n, d.h, d.w, d.ha, d.wa = x.n, x.h, x.w, x.ha, x.wa
+    d.cin, d.cout = cin, cout
+    d.x = x.view(x_coff)
+    d.y = y.view(y_coff)
+    d.y2 = y2.view(y2_coff) if y2 is not None else _NULL_VIEW
+    d.r1 = r1.view(r1_coff) if r1 is not None else _NULL_VIEW
+    d.r2 = r2.view(r2_coff) if r2 is not None else _NULL_VIEW
+    d.wpack = wpack.data_ptr()
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.slope, d.s1, d.s2, d.shuffle = slope, s1, s2, shuffle
+    check(_lib.load().isr_conv3x3_fwd(ctypes.byref(d), _stream()), "isr_conv3x3_fwd")
+
+
+def head9x9(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor | None, y: ActBuffer, *,
+            slope: float, y2: ActBuffer | None = None, y2_coff: int = 0,
+            mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)) -> None:
+    """9x9 head conv on an NCHW fp32 (normalised) or uint8 (raw) image."""
+    _require_gpu(x, "head9x9")
+    x = x.contiguous()
+    d = IsrHeadDesc()
+    d.n, d.h, d.w, d.ha, d.wa = y.n, y.h, y.w, y.ha, y.wa
+    d.cout = 64
+    d.x = x.data_ptr()
+    if x.dtype == torch.uint8:
+        d.x_u8 = 1
+    elif x.dtype == torch.float32:
+        d.x_u8 = 0
+    else:
+        raise TypeError(f"head9x9: input must be float32 or uint8, got {x.dtype}")
+    for i in range(3):
+        d.mean[i] = float(mean[i])
+        d.inv_std[i] = 1.0 / float(std[i])
+    d.y = y.view(0)
+    d.y2 = y2.view(y2_coff) if y2 is not None else _NULL_VIEW
+    d.wpack = wpack.data_ptr()
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.slope = slope
+    check(_lib.load().isr_head9x9_fwd(ctypes.byref(d), _stream()), "isr_head9x9_fwd")
+
+
+def tail9x9(x: ActBuffer, wpack: torch.Tensor, bias: torch.Tensor | None, out: torch.Tensor) -> None:
+    """out (NCHW [n,3,h,w], fp32 or uint8) = tanh(conv9x9(x) + bias) (→ uint8 image)."""
+    _require_gpu(out, "tail9x9")
+    if out.dtype not in (torch.float32, torch.uint8) or not out.is_contiguous():
+        raise TypeError("tail9x9: out must be a contiguous float32 or uint8 tensor")
+    if tuple(out.shape) != (x.n, 3, x.h, x.w):
+        raise ValueError(f"tail9x9: out shape {tuple(out.shape)} != {(x.n, 3, x.h, x.w)}")
+    d = IsrTailDesc()
+    d.n, d.h, d.w, d.ha, d.wa = x.n, x.h, x.w, x.ha, x.wa
+    d.cin = 64
+    d.x = x.view(0)
+    d.wpack = wpack.data_ptr()
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.y = out.data_ptr()
+    d.y_u8 = 1 if out.dtype == torch.uint8 else 0
+    check(_lib.load().isr_tail9x9_fwd(ctypes.byref(d), _stream()), "isr_tail9x9_fwd")

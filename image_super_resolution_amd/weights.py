@@ -1,0 +1,89 @@
+"""Deterministic synthetic weights and inputs.
+
+There are no trained SR weights anywhere (the shipped
+model.pt is a denoiser) and no network, so every parity fixture, test and the
+benchmark use weights produced here.  Each tensor is drawn from numpy's PCG64
+seeded by (seed, crc32 of its state_dict key), so the values depend only on
+the key, the shape and the seed — not on module construction order or torch's
+RNG — and the golden-vector script can install exactly the same weights into
+the reference modules.
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import torch
+
+
+def _rng(seed: int, key: str) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64([seed & 0xFFFFFFFF, zlib.crc32(key.encode())]))
+
+
+def synth_tensor(key: str, shape: tuple[int, ...], seed: int = 0) -> np.ndarray:
+    """fp32 array for state_dict entry `key` of `shape`."""
+    g = _rng(seed, key)
+    leaf = key.rsplit(".", 1)[-1]
+    if leaf == "num_batches_tracked":
+        return np.zeros(shape, dtype=np.int64)
+    parent = key.rsplit(".", 2)[-2] if key.count(".") >= 1 else ""
+    is_bn = parent in ("bn", "store_bn")
+    if is_bn:
+        if leaf == "weight":
+            return g.uniform(0.8, 1.2, shape).astype(np.float32)
+        if leaf == "bias":
+            return g.uniform(-0.1, 0.1, shape).astype(np.float32)
+        if leaf == "running_mean":
+            return g.uniform(-0.1, 0.1, shape).astype(np.float32)
+        if leaf == "running_var":
+            return g.uniform(0.5, 1.5, shape).astype(np.float32)
+    if leaf == "weight" and len(shape) >= 2:
+        fan_in = int(np.prod(shape[1:]))
+        # unit-variance pre-activations; He gain for the ReLU VGG stack so that
+        # conv5_4 features do not vanish
+        gain = 2.0 if "vgg" in key else 1.0
+        bound = np.sqrt(3.0 * gain / fan_in)
+        return g.uniform(-bound, bound, shape).astype(np.float32)
+    if leaf == "bias":
+        return g.uniform(-0.05, 0.05, shape).astype(np.float32)
+    return g.uniform(-0.1, 0.1, shape).astype(np.float32)
+
+
+def synth_state_dict(template: dict[str, torch.Tensor], seed: int = 0) -> dict[str, torch.Tensor]:
+    """Replace every entry of a state_dict template with deterministic values."""
+    out = {}
+    for k, v in template.items():
+        a = synth_tensor(k, tuple(v.shape), seed)
+        out[k] = torch.from_numpy(a).to(v.dtype) if v.is_floating_point() or v.dtype == torch.int64 else v.clone()
+    return out
+
+
+def synth_lr_batch(n: int, h: int, w: int, seed: int = 1234, scale: int = 4) -> tuple[torch.Tensor, torch.Tensor]:
+    """Smooth 'natural-ish' HR images and their LR counterparts.
+
+    HR [n,3,h*scale,w*scale] in [0,1]: bicubic upsampling of U[0,1] noise at
+    1/16 resolution; LR = antialiased bilinear x(1/scale) downsample of HR.
+    Returns (lr_unnormalised in [0,1], hr in [0,1]), both fp32 CPU.
+    """
+    import torch.nn.functional as F
+
+    hs, ws = h * scale, w * scale
+    hrs = []
+    for i in range(n):
+        g = torch.Generator().manual_seed(seed + i)
+        base = torch.rand(1, 3, max(2, hs // 16), max(2, ws // 16), generator=g)
+        hr = F.interpolate(base, size=(hs, ws), mode="bicubic", align_corners=False).clamp_(0, 1)
+        hrs.append(hr)
+    hr = torch.cat(hrs)
+    lr = F.interpolate(hr, size=(h, w), mode="bilinear", align_corners=False, antialias=True).clamp_(0, 1)
+    return lr, hr
+
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def normalize(x01: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD) -> torch.Tensor:
+    m = torch.tensor(mean, dtype=x01.dtype, device=x01.device).view(1, 3, 1, 1)
+    s = torch.tensor(std, dtype=x01.dtype, device=x01.device).view(1, 3, 1, 1)
+    return (x01 - m) / s

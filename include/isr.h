@@ -1,0 +1,125 @@
+/*
+ * isr.h — C-ABI of libisr.so, the MI355X (gfx950) kernels behind the
+ * image_super_resolution_amd drop-in.
+ *
+ * The reference (thnak/image_super_resolution) has no FFI/plugin layer: its hot
+ * path is torch.nn modules dispatching to ATen convolutions.  Each entry point
+ * below replaces one group of those module forwards (cited per function,
+ * paths relative to the reference root).  A host binds these with ctypes (see
+ * INTEGRATION.md); no torch types cross this boundary.
+ *
+ * Conventions
+ *  - Activations are NHWC bf16 in caller-owned device buffers laid out as
+ *    [N][hp][wp][cs] with a zero border of `pad` pixels on every side.  The
+ *    caller zero-fills a buffer once; kernels never write the border and write
+ *    exact zeros at computed positions outside the valid h x w region, so the
+ *    border / alignment slack always reads as the conv's zero padding.
+ *  - Computed regions are tile-aligned: ha % ISR_TILE_H == 0, wa % ISR_TILE_W == 0.
+ *  - The library never allocates, frees or synchronises; every call takes an
+ *    explicit stream and is hipGraph-capturable.
+ *  - Return 0 on success, a negative ISR_ERR_* otherwise; isr_last_error()
+ *    returns a thread-local message for the last failure.
+ */
+#ifndef ISR_H
+#define ISR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* isr_stream_t; /* == hipStream_t */
+
+#define ISR_OK 0
+#define ISR_ERR_BAD_DESC (-1)
+#define ISR_ERR_UNSUPPORTED (-2)
+#define ISR_ERR_LAUNCH (-3)
+
+#define ISR_TILE_H 16
+#define ISR_TILE_W 32
+
+/* A channel slice of an NHWC bf16 buffer [N][hp][wp][cs] with border `pad`.
+ * Interior pixel (n, y, x), channel c lives at
+ *   data + (((n*hp + y + pad) * wp + x + pad) * cs + coff + c) * 2 bytes. */
+typedef struct isr_view {
+    void* data;
+    int32_t hp, wp, cs, pad, coff;
+} isr_view;
+
+/* 3x3 stride-1 'same' convolution with fused epilogue:
+ *   v = act(conv(x, W) + bias);  v = v*s1 + r1 (if r1);  v = v*s2 + r2 (if r2)
+ *   store v to y (PixelShuffle(2)-permuted when shuffle == 2) and to y2 (if set).
+ * act is LeakyReLU(slope) (slope = 1 → identity, 0 → ReLU).
+ * Replaces: Conv._forward_impl (utils/models.py:97-98, BN folded by
+ * fuse_conv_and_bn :366-406), ConvWithoutBN._forward_impl (:195-196),
+ * the torch.cat chain + residual of RDB.forward (:265-271; the caller points
+ * y at a channel slice of the dense-block buffer), RRDB.forward (:316-317, as
+ * r2), ResNet/EResNet trunk add (:615, :647) and Scaler (:572-589: conv →
+ * PixelShuffle(2) → LeakyReLU via shuffle == 2). */
+typedef struct isr_conv_desc {
+    int32_t n, h, w;   /* batch; valid conv height/width (input == output size) */
+    int32_t ha, wa;    /* computed (tile-aligned) extent; ha % 16 == 0, wa % 32 == 0 */
+    int32_t cin, cout; /* cin % 32 == 0; cout == 32 or cout % 64 == 0 */
+    isr_view x;        /* input (cin channels from x.coff) */
+    isr_view y;        /* output; for shuffle == 2 its grid is (2h, 2w), cout/4 channels */
+    isr_view y2;       /* optional duplicate output (y2.data == NULL → none) */
+    isr_view r1, r2;   /* optional residuals (data == NULL → none), cout channels */
+    const void* wpack; /* from isr_pack_conv3x3 */
+    const float* bias; /* [cout] fp32 or NULL */
+    float slope, s1, s2;
+    int32_t shuffle;   /* 1 = plain store, 2 = PixelShuffle(2) store */
+} isr_conv_desc;
+
+/* 9x9 head conv, 3 → cout (=64) channels, input NCHW (fp32 already normalised,
+ * or uint8 with Normalize fused), + bias + LeakyReLU(slope), NHWC bf16 out.
+ * Replaces: ResNet.conv0 / EResNet.conv0 (utils/models.py:596, :625) and the
+ * Normalize of Model.init_normalize (:731-732; utils/datasets.py:65-71). */
+typedef struct isr_head_desc {
+    int32_t n, h, w, ha, wa;
+    int32_t cout;          /* 64 */
+    const void* x;         /* NCHW [n][3][h][w] */
+    int32_t x_u8;          /* 0: fp32 input used as is; 1: uint8, (v/255 - mean)/std fused */
+    float mean[3], inv_std[3];
+    isr_view y, y2;
+    const void* wpack;     /* from isr_pack_head9x9 */
+    const float* bias;     /* [cout] or NULL */
+    float slope;
+} isr_head_desc;
+
+/* 9x9 tail conv, cin (=64) → 3 channels, + bias + tanh, NCHW out (fp32, or
+ * uint8 with TanhToArrayImage fused: round_half_even((t+1)/2*255)).
+ * Replaces: ResNet.conv2 / EResNet.conv2 (utils/models.py:607, :636) and
+ * TanhToArrayImage.forward (:448-451). */
+typedef struct isr_tail_desc {
+    int32_t n, h, w, ha, wa; /* valid / computed extent of the tail (= output size) */
+    int32_t cin;             /* 64 */
+    isr_view x;              /* NHWC bf16, pad >= 4 */
+    const void* wpack;       /* from isr_pack_tail9x9 */
+    const float* bias;       /* [3] or NULL */
+    void* y;                 /* NCHW [n][3][h][w] */
+    int32_t y_u8;            /* 0: fp32 tanh output; 1: uint8 image */
+} isr_tail_desc;
+
+/* Weight packing (device fp32 OIHW → device bf16 kernel layout).  Replaces the
+ * one-off fuse step's weight preparation (utils/models.py:741-751); BN folding
+ * itself is done by the caller before packing. */
+size_t isr_conv3x3_packed_bytes(int32_t cout, int32_t cin);
+int isr_pack_conv3x3(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
+size_t isr_head9x9_packed_bytes(int32_t cout, int32_t cin);
+int isr_pack_head9x9(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
+size_t isr_tail9x9_packed_bytes(int32_t cout, int32_t cin);
+int isr_pack_tail9x9(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
+
+int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s);
+int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s);
+int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);
+
+const char* isr_last_error(void);
+int isr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ISR_H */

@@ -1,0 +1,177 @@
+"""HIP kernel numerics vs a plain PyTorch fp32 reference of the same op.
+
+Inputs and weights are rounded to bf16 first (the kernels' storage type), so
+the remaining difference is fp32 accumulation order plus one bf16 rounding of
+the output: tolerance |err| <= 1.5e-2 * max(1, |ref|) elementwise, and mean
+error < 2e-3.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def close(got, ref, tol=1.5e-2, mean_tol=2e-3):
+    err = (got - ref).abs()
+    lim = tol * torch.clamp(ref.abs(), min=1.0)
+    assert bool((err <= lim).all()), f"max err {err.max().item():.3e} (ref max {ref.abs().max().item():.3e})"
+    assert err.mean().item() < mean_tol, f"mean err {err.mean().item():.3e}"
+
+
+def lrelu(x, s):
+    return torch.where(x >= 0, x, x * s)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib(built_lib):
+    return built_lib
+
+
+def _mk(n, c, h, w, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(n, c, h, w, generator=g).to(DEV)
+
+
+def _w(cout, cin, k, seed, scale=None):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    s = scale if scale is not None else (1.0 / (cin * k * k)) ** 0.5
+    return (torch.rand(cout, cin, k, k, generator=g) * 2 - 1).mul(s * 3 ** 0.5).to(DEV)
+
+
+@pytest.mark.parametrize("n,cin,cout,h,w", [(1, 64, 32, 16, 32), (2, 96, 32, 20, 36), (1, 160, 32, 33, 65),
+                                            (2, 192, 64, 18, 40), (1, 64, 64, 7, 5), (1, 64, 128, 16, 32)])
+def test_conv3x3_plain(n, cin, cout, h, w):
+    from image_super_resolution_amd import ops
+    x = _mk(n, cin, h, w, 1)
+    W = _w(cout, cin, 3, 2)
+    b = torch.randn(cout, device=DEV) * 0.1
+    xb = ops.ActBuffer.from_nchw(x, pad=1)
+    yb = ops.ActBuffer.alloc(n, h, w, cout, 1, DEV)
+    ops.conv3x3(xb, cin, ops.pack_conv3x3(W), b, cout, yb, slope=0.01)
+    torch.cuda.synchronize()
+    ref = lrelu(F.conv2d(bf(x), bf(W), b, padding=1), 0.01)
+    close(yb.to_nchw(), ref)
+    # everything outside the valid region (border + alignment slack) must stay exactly zero
+    full = yb.t.float()
+    mask = torch.ones_like(full, dtype=torch.bool)
+    mask[:, 1:1 + h, 1:1 + w, :] = False
+    assert full[mask].abs().max().item() == 0.0
+
+
+def test_conv3x3_dense_slice_and_residuals():
+    """Growth conv into a channel slice + RDB/RRDB double-residual epilogue."""
+    from image_super_resolution_amd import ops
+    n, h, w = 2, 24, 40
+    buf = ops.ActBuffer.alloc(n, h, w, 192, 1, DEV)
+    x = _mk(n, 96, h, w, 3)
+    buf.t[:, 1:1 + h, 1:1 + w, :96] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    before = buf.t.clone()
+    W = _w(32, 96, 3, 4)
+    b = torch.randn(32, device=DEV) * 0.1
+    ops.conv3x3(buf, 96, ops.pack_conv3x3(W), b, 32, buf, y_coff=96, slope=0.01)
+    torch.cuda.synchronize()
+    ref = lrelu(F.conv2d(bf(x), bf(W), b, padding=1), 0.01)
+    close(buf.to_nchw(96, 128), ref)
+    assert torch.equal(buf.t[..., :96], before[..., :96]) and torch.equal(buf.t[..., 128:], before[..., 128:])
+
+    # final conv: y = ((conv + b) * 0.2 + r1) * 0.2 + r2, written in place over r2
+    W2 = _w(64, 192, 3, 5)
+    b2 = torch.randn(64, device=DEV) * 0.1
+    xin = bf(buf.to_nchw(0, 192))
+    r2buf = ops.ActBuffer.alloc(n, h, w, 192, 1, DEV)
+    r2 = _mk(n, 64, h, w, 6)
+    r2buf.t[:, 1:1 + h, 1:1 + w, :64] = r2.permute(0, 2, 3, 1).to(torch.bfloat16)
+    ops.conv3x3(buf, 192, ops.pack_conv3x3(W2), b2, 64, r2buf, slope=1.0, r1=buf, s1=0.2, r2=r2buf, s2=0.2)
+    torch.cuda.synchronize()
+    ref = ((F.conv2d(xin, bf(W2), b2, padding=1)) * 0.2 + xin[:, :64]) * 0.2 + bf(r2)
+    close(r2buf.to_nchw(0, 64), ref)
+
+
+def test_conv3x3_pixel_shuffle():
+    from image_super_resolution_amd import ops
+    n, h, w = 2, 20, 36
+    x = _mk(n, 64, h, w, 7)
+    W = _w(256, 64, 3, 8)
+    b = torch.randn(256, device=DEV) * 0.1
+    xb = ops.ActBuffer.from_nchw(x, pad=1)
+    yb = ops.ActBuffer.alloc(n, 2 * h, 2 * w, 64, 4, DEV, ha=2 * xb.ha, wa=2 * xb.wa)
+    ops.conv3x3(xb, 64, ops.pack_conv3x3(W), b, 256, yb, slope=0.01, shuffle=2)
+    torch.cuda.synchronize()
+    ref = lrelu(F.pixel_shuffle(F.conv2d(bf(x), bf(W), b, padding=1), 2), 0.01)
+    close(yb.to_nchw(), ref)
+    full = yb.t.float()
+    mask = torch.ones_like(full, dtype=torch.bool)
+    mask[:, 4:4 + 2 * h, 4:4 + 2 * w, :] = False
+    assert full[mask].abs().max().item() == 0.0
+
+
+def test_conv3x3_dual_output():
+    from image_super_resolution_amd import ops
+    x = _mk(1, 64, 16, 32, 9)
+    W = _w(64, 64, 3, 10)
+    xb = ops.ActBuffer.from_nchw(x, pad=1)
+    y1 = ops.ActBuffer.alloc(1, 16, 32, 64, 1, DEV)
+    y2 = ops.ActBuffer.alloc(1, 16, 32, 192, 1, DEV)
+    ops.conv3x3(xb, 64, ops.pack_conv3x3(W), None, 64, y1, slope=1.0, y2=y2)
+    torch.cuda.synchronize()
+    assert torch.equal(y1.to_nchw(), y2.to_nchw(0, 64))
+    close(y1.to_nchw(), F.conv2d(bf(x), bf(W), padding=1))
+
+
+@pytest.mark.parametrize("u8", [False, True])
+def test_head9x9(u8):
+    from image_super_resolution_amd import ops
+    from image_super_resolution_amd.weights import normalize
+    n, h, w = 2, 20, 36
+    g = torch.Generator().manual_seed(11)
+    img = torch.rand(n, 3, h, w, generator=g).to(DEV)
+    if u8:
+        x = (img * 255).to(torch.uint8)
+        xin = normalize(x.float() / 255.0)
+    else:
+        x = normalize(img)
+        xin = x
+    W = _w(64, 3, 9, 12)
+    b = torch.randn(64, device=DEV) * 0.1
+    y = ops.ActBuffer.alloc(n, h, w, 64, 1, DEV)
+    y2 = ops.ActBuffer.alloc(n, h, w, 192, 1, DEV)
+    ops.head9x9(x, ops.pack_head9x9(W), b, y, slope=0.2, y2=y2)
+    torch.cuda.synchronize()
+    ref = lrelu(F.conv2d(bf(xin), bf(W), b, padding=4), 0.2)
+    close(y.to_nchw(), ref)
+    assert torch.equal(y.to_nchw(), y2.to_nchw(0, 64))
+
+
+@pytest.mark.parametrize("u8", [False, True])
+def test_tail9x9(u8):
+    from image_super_resolution_amd import ops
+    n, h, w = 2, 40, 72
+    x = _mk(n, 64, h, w, 13) * 0.5
+    W = _w(3, 64, 9, 14)
+    b = torch.randn(3, device=DEV) * 0.1
+    xb = ops.ActBuffer.from_nchw(x, pad=4)
+    out = torch.empty(n, 3, h, w, device=DEV, dtype=torch.uint8 if u8 else torch.float32)
+    ops.tail9x9(xb, ops.pack_tail9x9(W), b, out)
+    torch.cuda.synchronize()
+    ref = torch.tanh(F.conv2d(bf(x), bf(W), b, padding=4))
+    if u8:
+        ref8 = (((ref + 1) / 2) * 255).round()
+        d = (out.float() - ref8).abs()
+        assert d.max().item() <= 1 and (d > 0).float().mean().item() < 0.02
+    else:
+        close(out, ref, tol=5e-3, mean_tol=5e-4)
+
+
+def test_bad_descriptor_raises():
+    from image_super_resolution_amd import ops, _lib
+    x = ops.ActBuffer.alloc(1, 16, 32, 48, 1, DEV)  # cin 48 not a multiple of 32
+    y = ops.ActBuffer.alloc(1, 16, 32, 64, 1, DEV)
+    with pytest.raises(_lib.IsrError, match="multiple of 32"):
+        ops.conv3x3(x, 48, torch.zeros(10, dtype=torch.bfloat16, device=DEV), None, 64, y)

@@ -1,0 +1,127 @@
+"""Pin the CPU oracle (oracle/ref_cpu.py) to golden vectors produced by the reference itself.
+
+The fixtures were made by tests/golden/make_golden.py, which runs
+thnak/image_super_resolution's own modules (utils/models.py, utils/loss.py,
+rs.py).  Weights are rebuilt here from image_super_resolution_amd.weights
+(same key / shape / seed), so a pass means the oracle reproduces the reference
+bit-for-bit up to fp32 reassociation.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import t
+from image_super_resolution_amd import models
+from image_super_resolution_amd.weights import synth_state_dict
+from oracle import ref_cpu as R
+
+torch.set_grad_enabled(False)
+
+
+def _sd(model, seed):
+    return synth_state_dict(model.state_dict(), seed)
+
+
+@pytest.mark.parametrize("name,ctor,enchant", [
+    ("gen_resnet_x4", lambda: models.ResNet(1, 0.2, scaleRate=4), False),
+    ("gen_resnet_x2", lambda: models.ResNet(1, 0.2, scaleRate=2), False),
+    ("gen_eresnet_x4", lambda: models.EResNet(2, 0.2, scaleRate=4), True),
+])
+def test_generator_matches_reference(golden, name, ctor, enchant):
+    g = golden(name)
+    m = ctor()
+    sd = _sd(m, int(g["seed"]))
+    y = R.generator(sd, t(g["x"]), num_blocks=R.count_blocks(sd), scale=int(g["scale"]), enchant=enchant)
+    np.testing.assert_allclose(y.numpy(), g["y"], rtol=0, atol=2e-5)
+    # Model.fuse equivalence (utils/models.py:741-751)
+    yf = R.generator(R.fuse_state_dict(sd), t(g["x"]), num_blocks=R.count_blocks(sd), scale=int(g["scale"]),
+                     enchant=enchant)
+    np.testing.assert_allclose(yf.numpy(), g["y_fused"], rtol=0, atol=2e-5)
+
+
+def test_model_u8_matches_reference(golden):
+    g = golden("model_u8")
+    sd = R.fuse_state_dict(_sd(models.ResNet(1, 0.2, scaleRate=4), int(g["seed"])))
+    y = R.model_u8(sd, t(g["x"]), num_blocks=1, scale=4)
+    d = (y.int() - t(g["y"]).int()).abs()
+    assert d.max().item() <= 1 and (d > 0).float().mean().item() < 1e-3
+
+
+def test_tiled_stitch_matches_rs_py(golden):
+    g = golden("tiled_u8")
+    sd = R.fuse_state_dict(_sd(models.ResNet(1, 0.2, scaleRate=4), int(g["seed"])))
+    out = R.tiled_u8(lambda w: R.model_u8(sd, w, num_blocks=1, scale=4), t(g["x"]), int(g["window"]))
+    assert tuple(out.shape) == g["y"].shape
+    d = (out.int() - t(g["y"]).int()).abs()
+    assert d.max().item() <= 1 and (d > 0).float().mean().item() < 1e-3
+
+
+def test_blocks_match_reference(golden):
+    g = golden("blocks")
+    x = t(g["x"])
+    sd = _sd(models.Conv(64, 32, 3, 1, None, act=torch.nn.LeakyReLU()), 10)
+    y = R.conv_unit({f"c.{k}": v for k, v in sd.items()}, "c", x, 0.01)
+    np.testing.assert_allclose(y.numpy(), g["conv"], atol=1e-5)
+    sd = _sd(models.RDB(64, 32, 3, torch.nn.LeakyReLU(), add_rate=0.2), 11)
+    np.testing.assert_allclose(R.rdb({f"b.{k}": v for k, v in sd.items()}, "b", x, 0.2).numpy(), g["rdb"],
+                               atol=1e-5)
+    sd = _sd(models.RRDB(64, 3, torch.nn.LeakyReLU(), add_rate=0.2), 12)
+    np.testing.assert_allclose(R.rrdb({f"b.{k}": v for k, v in sd.items()}, "b", x, 0.2).numpy(), g["rrdb"],
+                               atol=1e-5)
+    sd = _sd(models.Scaler(64, 64, 2, 3, torch.nn.LeakyReLU()), 13)
+    np.testing.assert_allclose(R.scaler({f"s.{k}": v for k, v in sd.items()}, "s", x).numpy(), g["scaler"],
+                               atol=1e-5)
+
+
+def test_train_step_grads_match_reference(golden):
+    """One MSE pre-training step in train mode (batch-stat BN), fp32 (train.py:52-63)."""
+    g = golden("train_step_x2")
+    m = models.ResNet(1, 0.2, scaleRate=2)
+    sd = _sd(m, int(g["seed"]))
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items() if v.is_floating_point() and "running" not in k}
+    full = dict(sd)
+    full.update(params)
+    with torch.enable_grad():
+        pred = R.generator(full, t(g["x"]), num_blocks=1, scale=2, train_bn=True)
+        loss = F.mse_loss(pred, t(g["target"]))
+        loss.backward()
+    np.testing.assert_allclose(pred.detach().numpy(), g["pred"], atol=2e-5)
+    np.testing.assert_allclose(loss.item(), float(g["loss"]), rtol=1e-5)
+    for k in g:
+        if k.startswith("grad:"):
+            ref = g[k]
+            got = params[k[5:]].grad.numpy()
+            np.testing.assert_allclose(got, ref, atol=1e-5 * max(1.0, np.abs(ref).max()), err_msg=k)
+    for k in g:
+        if k.startswith("stat:"):
+            np.testing.assert_allclose(full[k[5:]].numpy(), g[k], atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("which,before_act", [("postact", False), ("preact", True)])
+def test_vgg_losses_match_reference(golden, which, before_act):
+    g = golden(f"loss_vgg_{which}")
+    vgg_tmpl = {}
+    for idx, (kind, cin, cout) in enumerate(R.vgg19_features_cfg()[:R.truncate_index(5, 4) + (0 if before_act else 1)]):
+        if kind == "conv":
+            vgg_tmpl[f"truncated_vgg19.{idx}.weight"] = torch.empty(cout, cin, 3, 3)
+            vgg_tmpl[f"truncated_vgg19.{idx}.bias"] = torch.empty(cout)
+    sd = synth_state_dict(vgg_tmpl, int(g["seed"]))
+    sr = t(g["sr"]).requires_grad_(True)
+    feats = R.vgg_truncated(sd, sr, before_act=before_act)
+    np.testing.assert_allclose(feats.detach().numpy(), g["feats"], rtol=1e-4, atol=1e-5)
+    with torch.enable_grad():
+        perc, adv, content = R.content_loss(sd, sr, t(g["hr"]), t(g["sr_disc"]), before_act=before_act)
+        content.backward()
+    np.testing.assert_allclose(perc.item(), float(g["perceptual"]), rtol=1e-5)
+    np.testing.assert_allclose(adv.item(), float(g["adversarial"]), rtol=1e-6)
+    np.testing.assert_allclose(content.item(), float(g["content"]), rtol=1e-5)
+    gr = g["grad_sr"]
+    np.testing.assert_allclose(sr.grad.numpy(), gr, atol=1e-4 * np.abs(gr).max())
+    np.testing.assert_allclose(R.adv_loss(t(g["sr_disc"]), t(g["hr_disc"])).item(), float(g["d_loss"]), rtol=1e-6)
+
+
+def test_ema_decay_matches_reference(golden):
+    g = golden("ema")
+    for u, d in zip(g["updates"], g["decay"]):
+        assert abs(R.ema_decay(int(u), float(g["tau"])) - d) < 1e-12
