@@ -18,6 +18,7 @@ BatchNorm is folded into the conv (fuse_conv_and_bn, :366-406) at pack time.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass, field
 
 import torch
@@ -135,33 +136,98 @@ def rrdb_forward(blk, X: ActBuffer, Y: ActBuffer, Z: ActBuffer, add_rate: float,
     rdb_forward(blk[2], Z, X, add_rate, r2=X, s2=add_rate, slope=slope)
 
 
-def run_generator(gw: GeneratorWeights, x: torch.Tensor, *, out_u8: bool = False,
-                  mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)) -> torch.Tensor:
-    """x: NCHW [n,3,h,w] fp32 (normalised) or uint8 (Normalize fused) on the GPU."""
+class GeneratorPlan:
+    """Pre-built launch list of one generator forward for a fixed geometry.
+
+    Building ctypes descriptors costs tens of microseconds each in Python;
+    a forward has ~245 launches, so descriptors are built once per geometry
+    and only the input / output pointers are patched per call.  Each entry
+    carries a tag (kind, cin, cout) so callers can bracket the launches of
+    one kernel shape with HIP events (bench.py).
+    """
+
+    def __init__(self, gw: GeneratorWeights, n: int, h: int, w: int, device, x_u8: bool, out_u8: bool,
+                 mean, std):
+        self.key = (n, h, w, str(device), x_u8, out_u8, tuple(mean), tuple(std))
+        bufs = GeneratorBuffers(n, h, w, len(gw.scalers), device)
+        self.bufs = bufs
+        feat = bufs.feat
+        X, Y, Z = bufs.dense
+        lib = ops._lib.load()
+        conv, head, tail = lib.isr_conv3x3_fwd, lib.isr_head9x9_fwd, lib.isr_tail9x9_fwd
+        dummy_x = torch.empty((n, 3, h, w), dtype=torch.uint8 if x_u8 else torch.float32, device=device)
+        cur_h, cur_w = h * 2 ** len(gw.scalers), w * 2 ** len(gw.scalers)
+        self.out_shape = (n, 3, cur_h, cur_w)
+        self.out_dtype = torch.uint8 if out_u8 else torch.float32
+        dummy_out = torch.empty(self.out_shape, dtype=self.out_dtype, device=device)
+        self.head_desc = ops.head9x9_desc(dummy_x, gw.head.w, gw.head.b, feat, slope=gw.conv0_slope, y2=X,
+                                          mean=mean, std=std)
+        L = [(head, self.head_desc, ("head9x9", 3, 64))]
+
+        def c3(src, pc, dst, **kw):
+            L.append((conv, ops.conv3x3_desc(src, pc.cin, pc.w, pc.b, pc.cout, dst, **kw),
+                      ("conv3x3", pc.cin, pc.cout)))
+
+        ar = gw.add_rate
+        for blk in gw.rdb:
+            for r, (src, dst) in enumerate(((X, Y), (Y, Z), (Z, X))):
+                for k in range(4):
+                    c3(src, blk[r][k], src, y_coff=blk[r][k].cin, slope=LEAKY_DEFAULT)
+                extra = dict(r2=X, s2=ar) if r == 2 else {}
+                c3(src, blk[r][4], dst, slope=1.0, r1=src, s1=ar, **extra)
+        c3(X, gw.conv1, feat, slope=1.0, r1=feat, s1=1.0)
+        cur = feat
+        for s, pc in enumerate(gw.scalers):
+            c3(cur, pc, bufs.up[s], slope=LEAKY_DEFAULT, shuffle=2)
+            cur = bufs.up[s]
+        self.tail_desc = ops.tail9x9_desc(cur, gw.tail.w, gw.tail.b, dummy_out)
+        L.append((tail, self.tail_desc, ("tail9x9", 64, 3)))
+        self.launches = L
+        self._keep = (dummy_x, dummy_out)
+
+    def run(self, x: torch.Tensor, out: torch.Tensor, around=None) -> torch.Tensor:
+        """Launch the forward on the current stream.  `around(tag)` may return
+        (start_event, end_event) to bracket that launch."""
+        if tuple(out.shape) != self.out_shape or out.dtype != self.out_dtype or not out.is_contiguous():
+            raise ValueError("GeneratorPlan.run: output tensor does not match the plan")
+        if not x.is_contiguous():
+            raise ValueError("GeneratorPlan.run: input must be contiguous NCHW")
+        self.head_desc.x = x.data_ptr()
+        self.tail_desc.y = out.data_ptr()
+        stream = ops._stream()
+        byref = ctypes.byref
+        for fn, d, tag in self.launches:
+            ev = around(tag) if around is not None else None
+            if ev is not None:
+                ev[0].record()
+            rc = fn(byref(d), stream)
+            if rc != 0:
+                ops.check(rc, f"{tag[0]} launch")
+            if ev is not None:
+                ev[1].record()
+        return out
+
+
+def get_plan(gw: GeneratorWeights, x: torch.Tensor, out_u8: bool, mean, std) -> GeneratorPlan:
     n, c, h, w = x.shape
     if c != 3:
         raise ValueError(f"generator expects 3 input channels, got {c}")
-    key = (n, h, w, x.device)
-    bufs = gw.buffers.get(key)
-    if bufs is None:
-        bufs = GeneratorBuffers(n, h, w, len(gw.scalers), x.device)
-        gw.buffers = {key: bufs}  # keep one geometry resident
-    feat = bufs.feat
-    X, Y, Z = bufs.dense
-    ar = gw.add_rate
-    ops.head9x9(x, gw.head.w, gw.head.b, feat, slope=gw.conv0_slope, y2=X, mean=mean, std=std)
-    for blk in gw.rdb:
-        rrdb_forward(blk, X, Y, Z, ar)
-    pc = gw.conv1
-    ops.conv3x3(X, pc.cin, pc.w, pc.b, pc.cout, feat, slope=1.0, r1=feat, s1=1.0)
-    cur = feat
-    for s, pc in enumerate(gw.scalers):
-        nxt = bufs.up[s]
-        ops.conv3x3(cur, pc.cin, pc.w, pc.b, pc.cout, nxt, slope=LEAKY_DEFAULT, shuffle=2)
-        cur = nxt
-    out = torch.empty((n, 3, cur.h, cur.w), dtype=torch.uint8 if out_u8 else torch.float32, device=x.device)
-    ops.tail9x9(cur, gw.tail.w, gw.tail.b, out)
-    return out
+    key = (n, h, w, str(x.device), x.dtype == torch.uint8, out_u8, tuple(mean), tuple(std))
+    plan = gw.buffers.get("plan")
+    if plan is None or plan.key != key:
+        gw.buffers["plan"] = None  # free the previous geometry first
+        plan = GeneratorPlan(gw, n, h, w, x.device, x.dtype == torch.uint8, out_u8, mean, std)
+        gw.buffers["plan"] = plan
+    return plan
+
+
+def run_generator(gw: GeneratorWeights, x: torch.Tensor, *, out_u8: bool = False,
+                  mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)) -> torch.Tensor:
+    """x: NCHW [n,3,h,w] fp32 (normalised) or uint8 (Normalize fused) on the GPU."""
+    x = x.contiguous()
+    plan = get_plan(gw, x, out_u8, mean, std)
+    out = torch.empty(plan.out_shape, dtype=plan.out_dtype, device=x.device)
+    return plan.run(x, out)
 
 
 def generator_flops(h: int, w: int, num_blocks: int = 16, n_scalers: int = 2) -> float:

@@ -112,12 +112,12 @@ def pack_tail9x9(w: torch.Tensor) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------- launches
-def conv3x3(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor | None, cout: int,
-            y: ActBuffer, *, x_coff: int = 0, y_coff: int = 0, slope: float = 1.0,
-            r1: ActBuffer | None = None, r1_coff: int = 0, s1: float = 1.0,
-            r2: ActBuffer | None = None, r2_coff: int = 0, s2: float = 1.0,
-            y2: ActBuffer | None = None, y2_coff: int = 0, shuffle: int = 1) -> None:
-    """y[..., y_coff:y_coff+cout] = epilogue(conv3x3(x[..., x_coff:x_coff+cin]))."""
+def conv3x3_desc(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor | None, cout: int,
+                 y: ActBuffer, *, x_coff: int = 0, y_coff: int = 0, slope: float = 1.0,
+                 r1: ActBuffer | None = None, r1_coff: int = 0, s1: float = 1.0,
+                 r2: ActBuffer | None = None, r2_coff: int = 0, s2: float = 1.0,
+                 y2: ActBuffer | None = None, y2_coff: int = 0, shuffle: int = 1) -> IsrConvDesc:
+    """Descriptor for y[..., y_coff:y_coff+cout] = epilogue(conv3x3(x[..., x_coff:x_coff+cin]))."""
     d = IsrConvDesc()
     d.n, d.h, d.w, d.ha, d.wa = x.n, x.h, x.w, x.ha, x.wa
     d.cin, d.cout = cin, cout
@@ -129,15 +129,25 @@ def conv3x3(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor | No
     d.wpack = wpack.data_ptr()
     d.bias = bias.data_ptr() if bias is not None else None
     d.slope, d.s1, d.s2, d.shuffle = slope, s1, s2, shuffle
+    return d
+
+
+def launch_conv3x3(d: IsrConvDesc) -> None:
     check(_lib.load().isr_conv3x3_fwd(ctypes.byref(d), _stream()), "isr_conv3x3_fwd")
 
 
-def head9x9(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor | None, y: ActBuffer, *,
-            slope: float, y2: ActBuffer | None = None, y2_coff: int = 0,
-            mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)) -> None:
-    """9x9 head conv on an NCHW fp32 (normalised) or uint8 (raw) image."""
+def conv3x3(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor | None, cout: int,
+            y: ActBuffer, **kw) -> None:
+    """y[..., y_coff:y_coff+cout] = epilogue(conv3x3(x[..., x_coff:x_coff+cin]))."""
+    launch_conv3x3(conv3x3_desc(x, cin, wpack, bias, cout, y, **kw))
+
+
+def head9x9_desc(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor | None, y: ActBuffer, *,
+                 slope: float, y2: ActBuffer | None = None, y2_coff: int = 0,
+                 mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)) -> IsrHeadDesc:
     _require_gpu(x, "head9x9")
-    x = x.contiguous()
+    if not x.is_contiguous():
+        raise ValueError("head9x9: input must be contiguous NCHW")
     d = IsrHeadDesc()
     d.n, d.h, d.w, d.ha, d.wa = y.n, y.h, y.w, y.ha, y.wa
     d.cout = 64
@@ -156,11 +166,19 @@ def head9x9(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor | None, y: 
     d.wpack = wpack.data_ptr()
     d.bias = bias.data_ptr() if bias is not None else None
     d.slope = slope
+    return d
+
+
+def launch_head9x9(d: IsrHeadDesc) -> None:
     check(_lib.load().isr_head9x9_fwd(ctypes.byref(d), _stream()), "isr_head9x9_fwd")
 
 
-def tail9x9(x: ActBuffer, wpack: torch.Tensor, bias: torch.Tensor | None, out: torch.Tensor) -> None:
-    """out (NCHW [n,3,h,w], fp32 or uint8) = tanh(conv9x9(x) + bias) (→ uint8 image)."""
+def head9x9(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor | None, y: ActBuffer, **kw) -> None:
+    """9x9 head conv on an NCHW fp32 (normalised) or uint8 (raw) image."""
+    launch_head9x9(head9x9_desc(x.contiguous(), wpack, bias, y, **kw))
+
+
+def tail9x9_desc(x: ActBuffer, wpack: torch.Tensor, bias: torch.Tensor | None, out: torch.Tensor) -> IsrTailDesc:
     _require_gpu(out, "tail9x9")
     if out.dtype not in (torch.float32, torch.uint8) or not out.is_contiguous():
         raise TypeError("tail9x9: out must be a contiguous float32 or uint8 tensor")
@@ -174,4 +192,13 @@ def tail9x9(x: ActBuffer, wpack: torch.Tensor, bias: torch.Tensor | None, out: t
     d.bias = bias.data_ptr() if bias is not None else None
     d.y = out.data_ptr()
     d.y_u8 = 1 if out.dtype == torch.uint8 else 0
+    return d
+
+
+def launch_tail9x9(d: IsrTailDesc) -> None:
     check(_lib.load().isr_tail9x9_fwd(ctypes.byref(d), _stream()), "isr_tail9x9_fwd")
+
+
+def tail9x9(x: ActBuffer, wpack: torch.Tensor, bias: torch.Tensor | None, out: torch.Tensor) -> None:
+    """out (NCHW [n,3,h,w], fp32 or uint8) = tanh(conv9x9(x) + bias) (→ uint8 image)."""
+    launch_tail9x9(tail9x9_desc(x, wpack, bias, out))
