@@ -52,6 +52,7 @@ SIGNATURES = {
     "isr_tail9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),
     "isr_pack_tail9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "isr_conv3x3_fwd": (c_int32, [POINTER(IsrConvDesc), c_void_p]),
+    "isr_conv3x3_fwd_variant": (c_int32, [POINTER(IsrConvDesc), c_int32, c_void_p]),
     "isr_head9x9_fwd": (c_int32, [POINTER(IsrHeadDesc), c_void_p]),
     "isr_tail9x9_fwd": (c_int32, [POINTER(IsrTailDesc), c_void_p]),
     "isr_last_error": (ctypes.c_char_p, []),

@@ -9,7 +9,7 @@
 
 namespace isr {
 int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s);
-int conv3x3_cout_tile(int cout);
+int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s);
 size_t conv3x3_packed_bytes(int cout, int cin);
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s);
@@ -89,7 +89,7 @@ int isr_pack_tail9x9(const float* w, void* packed, int32_t cout, int32_t cin, is
     return launched(isr::tail9x9_pack(w, packed, cout, cin, (hipStream_t)s), "pack_tail9x9");
 }
 
-int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s) {
+static int conv3x3_validate(const isr_conv_desc* d) {
     if (!d) return fail(ISR_ERR_BAD_DESC, "conv3x3: null descriptor");
     if (d->n <= 0 || d->h <= 0 || d->w <= 0) return fail(ISR_ERR_BAD_DESC, "conv3x3: empty problem n=%d h=%d w=%d", d->n, d->h, d->w);
     if (d->ha % ISR_TILE_H || d->wa % ISR_TILE_W || d->ha < d->h || d->wa < d->w)
@@ -113,7 +113,21 @@ int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s) {
         if (d->r2.data && !view_ok(d->r2, d->ha, d->wa, 0, d->cout, "conv3x3.r2", 1)) return ISR_ERR_BAD_DESC;
     }
     if (d->bias && ((uintptr_t)d->bias % 16)) return fail(ISR_ERR_BAD_DESC, "conv3x3: bias must be 16-byte aligned");
+    return ISR_OK;
+}
+
+int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s) {
+    int rc = conv3x3_validate(d);
+    if (rc != ISR_OK) return rc;
     return launched(isr::conv3x3_fwd_dispatch(d, (hipStream_t)s), "conv3x3");
+}
+
+int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_t s) {
+    int rc = conv3x3_validate(d);
+    if (rc != ISR_OK) return rc;
+    rc = isr::conv3x3_fwd_variant(d, variant, (hipStream_t)s);
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: variant %d not available for cout %d / cin %d", variant, d->cout, d->cin);
+    return launched(rc, "conv3x3");
 }
 
 int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s) {

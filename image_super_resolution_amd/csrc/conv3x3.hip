@@ -10,54 +10,57 @@
 // channels.  Wave w owns rows [w*R, w*R+R).  GEMM view per block:
 //   M = 32 pixels of one row (one MFMA row-fragment per output row),
 //   N = CT output channels (NF fragments of 32),
-//   K = 9 taps x Cin, walked in chunks of 32 input channels.
-// Per chunk the (TH+2) x 34 x 32ch halo image and the chunk's packed weights
-// are copied global → LDS with global_load_lds_dwordx4 (double-buffered), then
-// each wave walks (dx, k-step) and re-uses every A fragment (one input row)
-// for the up-to-3 output rows (dy taps) that read it: R+2 A reads feed 3*R*NF
-// MFMAs.  The epilogue transposes the accumulators through LDS so that every
-// lane stores 16 contiguous bytes (8 channels) of one pixel.
+//   K = 9 taps x Cin, walked in chunks of KC (16 or 32) input channels.
+// Per chunk the (TH+2) x 34 x KC halo image and the chunk's packed weights are
+// copied global → LDS with global_load_lds_dwordx4 into an NST-deep ring; each
+// wave walks (k-step, dx) and re-uses every A fragment (one input row) for the
+// up-to-3 output rows (dy taps) that read it: R+2 A reads feed 3*R*NF MFMAs.
+// The epilogue transposes one output row at a time through LDS so that every
+// lane stores 16 contiguous bytes (8 channels) of one pixel, keeping the LDS
+// footprint small enough for two blocks per CU.
 #include "isr_common.h"
 
 namespace isr {
 
-template <int R, int WM, int NF>
+template <int R_, int WM_, int NF_, int KC_, int NST_>
 struct C3 {
+    static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
     static constexpr int TH = R * WM;
     static constexpr int TW = 32;
     static constexpr int HR = TH + 2;  // halo rows
     static constexpr int HC = TW + 2;  // halo cols
     static constexpr int CT = NF * 32; // output channels per block
-    static constexpr int KC = 32;      // input channels per chunk
-    static constexpr int HALO_UNITS = HR * HC * 4;
+    static constexpr int UPP = KC / 8; // 16-byte units per halo pixel
+    static constexpr int KS = KC / 16; // MFMA k-steps per chunk
+    static constexpr int HALO_UNITS = HR * HC * UPP;
     static constexpr int HALO_INSTR = (HALO_UNITS + 63) / 64;
-    static constexpr int HALO_BYTES = HALO_INSTR * 1024;
-    static constexpr int W_UNITS = 9 * 2 * CT * 2; // [tap][ks][n][hpos] x 16 B
+    static constexpr int W_UNITS = 9 * KS * CT * 2; // [c16][tap][n][hpos] x 16 B
     static constexpr int W_INSTR = W_UNITS / 64;
-    static constexpr int W_BYTES = W_UNITS * 16;
-    static constexpr int STAGE = HALO_BYTES + W_BYTES;
-    static constexpr int NT = 64 * WM;
     static constexpr int INSTR = HALO_INSTR + W_INSTR;
-    static constexpr int IPW = (INSTR + WM - 1) / WM; // glds instructions per wave per chunk
+    static constexpr int IPW = (INSTR + WM - 1) / WM; // glds per wave per chunk (uniform)
+    static constexpr int STAGE = IPW * WM * 1024;
+    static constexpr int NT = 64 * WM;
     static constexpr int EPS = CT + 4;                // floats per pixel in the epilogue image
-    static constexpr int EP_BYTES = WM * R * 32 * EPS * 4;
-    static constexpr int LDS = (2 * STAGE > EP_BYTES) ? 2 * STAGE : EP_BYTES;
+    static constexpr int EP_BYTES = WM * 32 * EPS * 4; // one output row per wave at a time
+    static constexpr int LDS = (NST * STAGE > EP_BYTES) ? NST * STAGE : EP_BYTES;
+    static constexpr int OCC = (163840 / LDS) * WM / 4 >= 2 ? 2 : 1; // waves per SIMD to budget registers for
     static_assert(W_UNITS % 64 == 0, "weight stage must be whole glds instructions");
     static_assert(LDS <= 163840, "LDS budget");
+    static_assert(KC == 16 || KC == 32, "chunk width");
 };
 
-// Packed weight layout for cout tile `ct`, input chunk `ch`:
-//   [tap 9][ks 2][n CT][hpos 2][8 bf16]  (one contiguous W_BYTES block)
-// element (tap=dy*3+dx, ks, n, hpos, e) = W[ct*CT+n][ch*32 + ks*16 + h*8 + e][dy][dx],
-// h = hpos ^ ((n >> 3) & 1) (bank swizzle of the B-fragment ds_read_b128).
-__device__ __forceinline__ int wunit(int tap, int ks, int n, int h, int CT) {
-    return ((tap * 2 + ks) * CT + n) * 2 + (h ^ ((n >> 3) & 1));
+__device__ __forceinline__ int swz_unit(int q, int c, int upp) {
+    // halo image: UPP units of 16 B per pixel, XOR-swizzled so that the 32
+    // consecutive pixels of an A-fragment ds_read_b128 hit 16 distinct slots.
+    return upp == 4 ? q * 4 + (c ^ ((q >> 2) & 3)) : q * 2 + (c ^ ((q >> 3) & 1));
 }
 
-template <int R, int WM, int NF>
-__global__ __launch_bounds__(64 * WM) void conv3x3_fwd_kernel(isr_conv_desc d) {
-    using C = C3<R, WM, NF>;
+// Packed weights (isr_pack_conv3x3): [c16 = cin/16][tap 9][cout][hpos 2][8 bf16],
+// element = W[n][c16*16 + h*8 + e][tap], h = hpos ^ ((n >> 3) & 1).
+template <class C>
+__global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_desc d) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int R = C::R, NF = C::NF, WM = C::WM;
 
     const int nct = d.cout / C::CT;
     const int img = blockIdx.z / nct;
@@ -72,9 +75,10 @@ __global__ __launch_bounds__(64 * WM) void conv3x3_fwd_kernel(isr_conv_desc d) {
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
     const char* xbase = view_px(d.x, img, y0 - 1, x0 - 1);
-    const char* wbase = (const char*)d.wpack + (size_t)ct * nchunks * C::W_BYTES;
+    const char* wbase = (const char*)d.wpack;
     const int xrow_bytes = d.x.wp * d.x.cs * 2;
     const int xpix_bytes = d.x.cs * 2;
+    const int wchunk_bytes = C::KS * 9 * d.cout * 32;
     uint32_t off[C::IPW];
 #pragma unroll
     for (int k = 0; k < C::IPW; ++k) {
@@ -83,15 +87,18 @@ __global__ __launch_bounds__(64 * WM) void conv3x3_fwd_kernel(isr_conv_desc d) {
         if (j < C::HALO_INSTR) {
             const int u = j * 64 + lane;
             if (u < C::HALO_UNITS) {
-                const int q = u >> 2;
-                const int cpos = u & 3;
+                const int q = u / C::UPP;
+                const int cpos = u - q * C::UPP;
                 const int row = q / C::HC;
                 const int col = q - row * C::HC;
-                const int c = cpos ^ ((q >> 2) & 3);
+                const int c = C::UPP == 4 ? (cpos ^ ((q >> 2) & 3)) : (cpos ^ ((q >> 3) & 1));
                 o = (uint32_t)(row * xrow_bytes + col * xpix_bytes + c * 16);
             }
-        } else {
-            o = (uint32_t)((j - C::HALO_INSTR) * 1024 + lane * 16);
+        } else if (j < C::INSTR) {
+            const int u = (j - C::HALO_INSTR) * 64 + lane;
+            const int seg = u / (C::CT * 2); // (c16l, tap)
+            const int rem = u - seg * (C::CT * 2);
+            o = (uint32_t)((seg * d.cout + ct * C::CT) * 32 + rem * 16);
         }
         off[k] = o;
     }
@@ -99,14 +106,12 @@ __global__ __launch_bounds__(64 * WM) void conv3x3_fwd_kernel(isr_conv_desc d) {
     auto stage = [&](int chunk, int buf) {
         char* dst = smem + buf * C::STAGE;
         const char* xs = xbase + chunk * (C::KC * 2);
-        const char* ws = wbase + (size_t)chunk * C::W_BYTES;
+        const char* ws = wbase + (size_t)chunk * wchunk_bytes;
 #pragma unroll
         for (int k = 0; k < C::IPW; ++k) {
             const int j = wave + WM * k;
-            if (j < C::INSTR) {
-                const char* src = (j < C::HALO_INSTR ? xs : ws) + off[k];
-                glds16(src, dst + j * 1024);
-            }
+            const char* src = (j < C::HALO_INSTR ? xs : ws) + off[k];
+            glds16(src, dst + j * 1024);
         }
     };
 
@@ -118,31 +123,46 @@ __global__ __launch_bounds__(64 * WM) void conv3x3_fwd_kernel(isr_conv_desc d) {
 #pragma unroll
             for (int g = 0; g < 16; ++g) acc[r][f][g] = 0.f;
 
-    stage(0, 0);
-    wait_vm0();
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < C::NST - 1; ++s)
+        if (s < nchunks) stage(s, s);
 
     const int qw = wave * R * C::HC + l31; // halo pixel of (row w*R, col l31)
     for (int chunk = 0; chunk < nchunks; ++chunk) {
-        const int buf = chunk & 1;
-        if (chunk + 1 < nchunks) stage(chunk + 1, buf ^ 1);
-        const char* hs = smem + buf * C::STAGE;
-        const char* ws = hs + C::HALO_BYTES;
+        // chunk `chunk` landed for this wave: younger chunks in flight = min(NST-2, nchunks-1-chunk)
+        if constexpr (C::NST >= 3) {
+            if (chunk + C::NST - 2 < nchunks) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((C::NST - 2) * C::IPW) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (chunk + C::NST - 1 < nchunks) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+
+        const char* hs = smem + (chunk % C::NST) * C::STAGE;
+        const char* ws = hs + C::HALO_INSTR * 1024;
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
+        for (int ks = 0; ks < C::KS; ++ks) {
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
+            for (int dx = 0; dx < 3; ++dx) {
                 bf16x8 b[3][NF];
 #pragma unroll
                 for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-                    for (int f = 0; f < NF; ++f)
-                        b[dy][f] = lds_read16(ws + wunit(dy * 3 + dx, ks, f * 32 + l31, hh, C::CT) * 16);
+                    for (int f = 0; f < NF; ++f) {
+                        const int n = f * 32 + l31;
+                        const int u = ((ks * 9 + dy * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
+                        b[dy][f] = lds_read16(ws + u * 16);
+                    }
                 const int c = 2 * ks + hh;
 #pragma unroll
                 for (int i = 0; i < R + 2; ++i) {
                     const int q = qw + i * C::HC + dx;
-                    const bf16x8 a = lds_read16(hs + halo_unit(q, c) * 16);
+                    const bf16x8 a = lds_read16(hs + swz_unit(q, c, C::UPP) * 16);
 #pragma unroll
                     for (int dy = 0; dy < 3; ++dy) {
                         const int r = i - dy;
@@ -154,79 +174,80 @@ __global__ __launch_bounds__(64 * WM) void conv3x3_fwd_kernel(isr_conv_desc d) {
                 }
             }
         }
-        wait_vm0();
-        __syncthreads();
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier(); // all waves done reading the ring before it becomes the epilogue image
 
-    // ---- epilogue: accumulators → LDS [row][px][CT] fp32 → 8-channel stores
-    float* ep = reinterpret_cast<float*>(smem) + wave * (R * 32 * C::EPS);
+    // ---- epilogue, one output row per pass: acc → LDS [px][CT] fp32 → 8-channel stores
+    float* ep = reinterpret_cast<float*>(smem) + wave * (32 * C::EPS);
+    Epi e;
+    e.bias = d.bias; e.slope = d.slope; e.s1 = d.s1; e.s2 = d.s2;
+    e.y = d.y; e.y2 = d.y2; e.r1 = d.r1; e.r2 = d.r2; e.h = d.h; e.w = d.w;
+    constexpr int ITEMS = C::CT / 16; // per lane per row
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int r = 0; r < R; ++r) {
 #pragma unroll
         for (int f = 0; f < NF; ++f)
 #pragma unroll
             for (int g = 0; g < 16; ++g) {
                 const int px = (g & 3) + 8 * (g >> 2) + 4 * hh;
-                ep[(r * 32 + px) * C::EPS + f * 32 + l31] = acc[r][f][g];
+                ep[px * C::EPS + f * 32 + l31] = acc[r][f][g];
             }
-    __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0): this wave's LDS writes landed
-    __builtin_amdgcn_wave_barrier();
-
-    Epi e;
-    e.bias = d.bias; e.slope = d.slope; e.s1 = d.s1; e.s2 = d.s2;
-    e.y = d.y; e.y2 = d.y2; e.r1 = d.r1; e.r2 = d.r2; e.h = d.h; e.w = d.w;
-    constexpr int ITEMS = R * C::CT / 16; // per lane
-    if (d.shuffle == 2) {
-        // item → (row r, sub-row i, output col xo in [0,64), 8-channel group cg)
-        constexpr int CG = C::CT / 32;
-#pragma unroll 4
-        for (int it = 0; it < ITEMS; ++it) {
-            const int jj = lane + 64 * it;
-            const int cg = jj % CG;
-            const int rem = jj / CG;
-            const int xo = rem & 63;
-            const int si = (rem >> 6) & 1;
-            const int r = rem >> 7;
-            const int xc = xo >> 1, sj = xo & 1;
-            const int yy = y0 + wave * R + r;
-            const int xx = x0 + xc;
-            float v[8];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int yy = y0 + wave * R + r;
+        if (d.shuffle == 2) {
+            // item → (sub-row si, output col xo in [0,64), 8-channel group cg)
+            constexpr int CG = C::CT / 32;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int col = 4 * (cg * 8 + k) + 2 * si + sj;
-                v[k] = ep[(r * 32 + xc) * C::EPS + col] + (e.bias ? e.bias[ct * C::CT + col] : 0.f);
-                v[k] = v[k] >= 0.f ? v[k] : v[k] * e.slope;
-            }
-            if (!(yy < e.h && xx < e.w)) {
+            for (int it = 0; it < ITEMS; ++it) {
+                const int jj = lane + 64 * it;
+                const int cg = jj % CG;
+                const int rem = jj / CG;
+                const int xo = rem & 63;
+                const int si = rem >> 6;
+                const int xc = xo >> 1, sj = xo & 1;
+                const int xx = x0 + xc;
+                float v[8];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = 0.f;
+                for (int k = 0; k < 8; ++k) {
+                    const int col = 4 * (cg * 8 + k) + 2 * si + sj;
+                    v[k] = ep[xc * C::EPS + col] + (e.bias ? e.bias[ct * C::CT + col] : 0.f);
+                    v[k] = v[k] >= 0.f ? v[k] : v[k] * e.slope;
+                }
+                if (!(yy < e.h && xx < e.w)) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) v[k] = 0.f;
+                }
+                char* dst = view_px(e.y, img, 2 * yy + si, 2 * x0 + xo) + (ct * (C::CT / 4) + cg * 8) * 2;
+                store8_bf16(dst, v);
             }
-            char* dst = view_px(e.y, img, 2 * yy + si, 2 * x0 + xo) + (ct * (C::CT / 4) + cg * 8) * 2;
-            store8_bf16(dst, v);
+        } else {
+            constexpr int CG = C::CT / 8;
+#pragma unroll
+            for (int it = 0; it < ITEMS; ++it) {
+                const int jj = lane + 64 * it;
+                const int cg = jj % CG;
+                const int px = jj / CG;
+                float v[8];
+                const float* src = ep + px * C::EPS + cg * 8;
+                f32x4 a0 = *reinterpret_cast<const f32x4*>(src);
+                f32x4 a1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { v[k] = a0[k]; v[4 + k] = a1[k]; }
+                epi_plain8(e, v, img, yy, x0 + px, ct * C::CT + cg * 8);
+            }
         }
-    } else {
-        constexpr int CG = C::CT / 8;
-#pragma unroll 4
-        for (int it = 0; it < ITEMS; ++it) {
-            const int jj = lane + 64 * it;
-            const int cg = jj % CG;
-            const int p = jj / CG;
-            const int r = p >> 5, px = p & 31;
-            float v[8];
-            const float* src = ep + (r * 32 + px) * C::EPS + cg * 8;
-            f32x4 a0 = *reinterpret_cast<const f32x4*>(src);
-            f32x4 a1 = *reinterpret_cast<const f32x4*>(src + 4);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) { v[k] = a0[k]; v[4 + k] = a1[k]; }
-            epi_plain8(e, v, img, y0 + wave * R + r, x0 + px, ct * C::CT + cg * 8);
-        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
-template <int R, int WM, int NF>
+template <class C>
 static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
-    using C = C3<R, WM, NF>;
-    auto kern = conv3x3_fwd_kernel<R, WM, NF>;
+    if (d->cout % C::CT) return -2;
+    if (d->cin % C::KC) return -2;
+    auto kern = conv3x3_fwd_kernel<C>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
@@ -237,42 +258,60 @@ static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) {
-    if (d->cout == 32) return launch3x3<4, 4, 1>(d, s);
-    return launch3x3<4, 4, 2>(d, s);
+// Variant table: the production choice per shape is variant 0; the others are
+// kept for on-device A/B tuning (isr_conv3x3_fwd_variant).
+using V_G0 = C3<2, 4, 1, 32, 2>;  // cout 32: TH 8, 80 KB → 2 blocks / CU (fastest, tools/tune_conv.py r1)
+using V_G1 = C3<4, 4, 1, 32, 2>;  // cout 32: 115 KB → 1 block / CU (first version)
+using V_G2 = C3<4, 4, 1, 16, 3>;  // cout 32: 3-deep ring
+using V_G3 = C3<4, 4, 1, 16, 2>;  // cout 32: 58 KB → 2 blocks / CU
+using V_W0 = C3<4, 4, 2, 16, 2>;  // cout %64: 80 KB → 2 blocks / CU (fastest, tools/tune_conv.py r1)
+using V_W1 = C3<4, 4, 2, 32, 2>;  // cout %64: 150 KB → 1 block / CU (round-1 baseline)
+using V_W2 = C3<2, 4, 2, 32, 2>;  // cout %64: TH 8
+using V_W3 = C3<4, 4, 2, 16, 3>;  // cout %64: 3-deep ring, KC 16
+
+int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
+    if (d->cout == 32) {
+        switch (variant) {
+            case 0: return launch3x3<V_G0>(d, s);
+            case 1: return launch3x3<V_G1>(d, s);
+            case 2: return launch3x3<V_G2>(d, s);
+            case 3: return launch3x3<V_G3>(d, s);
+        }
+        return -2;
+    }
+    switch (variant) {
+        case 0: return launch3x3<V_W0>(d, s);
+        case 1: return launch3x3<V_W1>(d, s);
+        case 2: return launch3x3<V_W2>(d, s);
+        case 3: return launch3x3<V_W3>(d, s);
+    }
+    return -2;
 }
 
-int conv3x3_cout_tile(int cout) { return cout == 32 ? 32 : 64; }
+int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) { return conv3x3_fwd_variant(d, 0, s); }
 
-// ---- weight packing: fp32 OIHW → bf16 [ct][chunk][tap][ks][n][hpos][8] ----
-__global__ void pack3x3_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin, int CT) {
-    const int nchunks = cin / 32;
-    const size_t per_block = (size_t)9 * 2 * CT * 16;
-    const size_t total = per_block * nchunks * (cout / CT);
+// ---- weight packing: fp32 OIHW → bf16 [c16][tap][cout][hpos][8] -----------
+__global__ void pack3x3_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
+    const size_t total = (size_t)cout * cin * 9;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
         size_t rem = idx;
         const int e = rem % 8; rem /= 8;
         const int hpos = rem % 2; rem /= 2;
-        const int n = rem % CT; rem /= CT;
-        const int ks = rem % 2; rem /= 2;
+        const int n = rem % cout; rem /= cout;
         const int tap = rem % 9; rem /= 9;
-        const int ch = rem % nchunks; rem /= nchunks;
-        const int ct = (int)rem;
+        const int c16 = (int)rem;
         const int h = hpos ^ ((n >> 3) & 1);
-        const int co = ct * CT + n;
-        const int ci = ch * 32 + ks * 16 + h * 8 + e;
-        const int dy = tap / 3, dx = tap % 3;
-        out[idx] = (__bf16)w[((size_t)co * cin + ci) * 9 + dy * 3 + dx];
+        const int ci = c16 * 16 + h * 8 + e;
+        out[idx] = (__bf16)w[((size_t)n * cin + ci) * 9 + tap];
     }
 }
 
 size_t conv3x3_packed_bytes(int cout, int cin) { return (size_t)cout * cin * 9 * 2; }
 
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s) {
-    const int CT = conv3x3_cout_tile(cout);
     const size_t total = conv3x3_packed_bytes(cout, cin) / 2;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    hipLaunchKernelGGL(pack3x3_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)out, cout, cin, CT);
+    hipLaunchKernelGGL(pack3x3_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)out, cout, cin);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
