@@ -22,9 +22,10 @@
 
 namespace isr {
 
-template <int R_, int WM_, int NF_, int KC_, int NST_>
+template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
+    static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol, unrolled chunk loop)
     static constexpr int TH = R * WM;
     static constexpr int TW = 32;
     static constexpr int HR = TH + 2;  // halo rows
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     const int lane = threadIdx.x & 63;
     const int l31 = lane & 31;
     const int hh = lane >> 5;
-    const int nchunks = d.cin / C::KC;
+    const int nchunks = C::CIN ? C::CIN / C::KC : d.cin / C::KC;
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
     const char* xbase = view_px(d.x, img, y0 - 1, x0 - 1);
@@ -265,6 +266,7 @@ using V_G1 = C3<4, 4, 1, 32, 2>;  // cout 32: 115 KB → 1 block / CU (first ver
 using V_G2 = C3<4, 4, 1, 16, 3>;  // cout 32: 3-deep ring
 using V_G3 = C3<4, 4, 1, 16, 2>;  // cout 32: 58 KB → 2 blocks / CU
 using V_W0 = C3<4, 4, 2, 16, 2>;  // cout %64: 80 KB → 2 blocks / CU (fastest, tools/tune_conv.py r1)
+using V_F0 = C3<4, 4, 2, 16, 2, 192>;  // RDB final conv 192→64: V_W0 with compile-time cin
 using V_W1 = C3<4, 4, 2, 32, 2>;  // cout %64: 150 KB → 1 block / CU (round-1 baseline)
 using V_W2 = C3<2, 4, 2, 32, 2>;  // cout %64: TH 8
 using V_W3 = C3<4, 4, 2, 16, 3>;  // cout %64: 3-deep ring, KC 16
@@ -280,7 +282,7 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
         return -2;
     }
     switch (variant) {
-        case 0: return launch3x3<V_W0>(d, s);
+        case 0: return d->cin == 192 ? launch3x3<V_F0>(d, s) : launch3x3<V_W0>(d, s);
         case 1: return launch3x3<V_W1>(d, s);
         case 2: return launch3x3<V_W2>(d, s);
         case 3: return launch3x3<V_W3>(d, s);

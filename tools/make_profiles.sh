@@ -1,0 +1,36 @@
+#!/bin/bash
+# Produce the round's committed profiles (run on the GPU box from the repo root):
+#   profiles/<R>_bench_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `python3 bench.py`
+#   profiles/<R>_pmc_summary.json         per-kernel PMC summary (tools/pmc_summary.py)
+#   profiles/<R>_pmc_traffic.json         HBM bytes per launch of the dominant kernel (read by bench.py)
+#   profiles/<R>_bench.json               the bench line after the traffic file exists
+# usage: tools/make_profiles.sh r01
+set -eu
+R=${1:-r01}
+export TMPDIR=/tmp
+P=gpurun_out/profiles_$R   # gpurun merges only gpurun_out/ back; copy into profiles/ afterwards
+mkdir -p $P
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench_$R -o bench -- \
+  python3 bench.py --round $R > gpurun_out/prof_bench_$R.json 2> gpurun_out/prof_bench_$R.err
+cp gpurun_out/prof_bench_$R/bench_kernel_stats.csv $P/${R}_bench_kernel_stats.csv
+bash tools/profile_pmc.sh gpurun_out/pmc_bench_$R bench.py --no-cpu-baseline --steps 5 --warmup 2 --round $R
+python3 tools/pmc_summary.py gpurun_out/pmc_bench_$R --json $P/${R}_pmc_summary.json > /dev/null
+python3 - "$R" "$P" <<'EOF'
+import json, sys
+R, P = sys.argv[1], sys.argv[2]
+rows = json.load(open(f"{P}/{R}_pmc_summary.json"))
+dom = [r for r in rows if "192>" in r["kernel"]]
+if dom:
+    r = dom[0]
+    out = {"kernel": r["kernel"], "grid": r["grid"], "dispatches": r["dispatches"],
+           "hbm_bytes_per_launch": r["hbm_bytes"], "hbm_read_bytes": r["hbm_read_bytes"],
+           "hbm_write_bytes": r["hbm_write_bytes"],
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, KiB -> bytes, FETCH_SIZE x2 "
+                     "(gfx950 wide-load correction, MI355X_MICROARCH.md §HBM); mean over dispatches; "
+                     "Infinity-Cache hits are included in these counters"}
+    json.dump(out, open(f"{P}/{R}_pmc_traffic.json", "w"), indent=1)
+    print("traffic", out["hbm_bytes_per_launch"])
+EOF
+cp $P/${R}_pmc_traffic.json profiles/ 2>/dev/null || true
+timeout -k 10 600 python3 bench.py --round $R > $P/${R}_bench.json 2> gpurun_out/bench_final_$R.err
+cat $P/${R}_bench.json

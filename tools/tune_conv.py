@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="0,1,2,3")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default="", help="comma list of CINxCOUT shapes, e.g. 160x32,192x64")
     args = ap.parse_args()
     lib = _lib.load()
     dev = "cuda"
@@ -35,6 +36,9 @@ def main():
     variants = [int(v) for v in args.variants.split(",")]
     shapes = [(64, 32, 1, hw), (96, 32, 1, hw), (128, 32, 1, hw), (160, 32, 1, hw), (192, 64, 1, hw),
               (64, 64, 1, hw), (64, 256, 2, hw), (64, 256, 2, 2 * hw)]
+    if args.only:
+        keep = {tuple(int(v) for v in s.split("x")) for s in args.only.split(",")}
+        shapes = [s for s in shapes if (s[0], s[1]) in keep]
     results = []
     for cin, cout, shuffle, s in shapes:
         g = torch.Generator().manual_seed(cin + cout)
