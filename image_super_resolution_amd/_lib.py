@@ -13,7 +13,7 @@ from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libisr.so"
 
-TILE_H = 16  # ISR_TILE_H
+TILE_H = 32  # ISR_TILE_H
 TILE_W = 32  # ISR_TILE_W
 
 

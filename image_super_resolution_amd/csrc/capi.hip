@@ -53,8 +53,9 @@ static bool view_ok(const isr_view& v, int ha, int wa, int halo, int ch, const c
         fail(ISR_ERR_BAD_DESC, "%s: channels [%d,%d) exceed stride %d", name, v.coff, v.coff + ch, v.cs);
         return false;
     }
-    if (align16 && ((v.cs % 8) || (v.coff % 8) || ((uintptr_t)v.data % 16))) {
-        fail(ISR_ERR_BAD_DESC, "%s: channel stride/offset must be multiples of 8 and data 16-byte aligned", name);
+    if (align16 && ((v.cs % 16) || (v.coff % 16) || ((uintptr_t)v.data % 16))) {
+        fail(ISR_ERR_BAD_DESC, "%s: channel count/offset must be multiples of 16 (channel-blocked layout) "
+             "and data 16-byte aligned", name);
         return false;
     }
     return true;

@@ -1,5 +1,5 @@
 // 3x3 stride-1 'same' convolution as an implicit GEMM on CDNA4 MFMA
-// (v_mfma_f32_32x32x16_bf16), NHWC bf16 activations, fp32 accumulation.
+// (v_mfma_f32_32x32x16_bf16), channel-blocked bf16 activations, fp32 accumulation.
 //
 // Replaces the ATen convolution behind Conv / ConvWithoutBN / RDB / RRDB /
 // Scaler of the reference (utils/models.py:75-111, 174-199, 245-271, 298-317,
@@ -7,17 +7,19 @@
 // add/mul and PixelShuffle, which all become the epilogue of one launch.
 //
 // Block tile: TH = R*WM output rows x 32 output columns x CT = NF*32 output
-// channels.  Wave w owns rows [w*R, w*R+R).  GEMM view per block:
+// channels; wave w owns rows [w*R, w*R+R).  GEMM view per block:
 //   M = 32 pixels of one row (one MFMA row-fragment per output row),
 //   N = CT output channels (NF fragments of 32),
 //   K = 9 taps x Cin, walked in chunks of KC (16 or 32) input channels.
-// Per chunk the (TH+2) x 34 x KC halo image and the chunk's packed weights are
-// copied global → LDS with global_load_lds_dwordx4 into an NST-deep ring; each
-// wave walks (k-step, dx) and re-uses every A fragment (one input row) for the
-// up-to-3 output rows (dy taps) that read it: R+2 A reads feed 3*R*NF MFMAs.
+// Activations are [N][C/16][H][W][16]: a K-chunk is KC/16 contiguous planes, so
+// each halo row of a chunk is one contiguous 34 x 32-byte run (whole cache
+// lines).  Per chunk the (TH+2) x 34 halo planes and the chunk's packed weights
+// are copied global → LDS with global_load_lds_dwordx4 into an NST-deep ring;
+// each wave walks (k-step, dx) and re-uses every A fragment (one input row) for
+// the up-to-3 output rows (dy taps) that read it: R+2 A reads feed 3*R*NF MFMAs.
 // The epilogue transposes one output row at a time through LDS so that every
-// lane stores 16 contiguous bytes (8 channels) of one pixel, keeping the LDS
-// footprint small enough for two blocks per CU.
+// lane stores 16 contiguous bytes (8 channels) of one pixel.
+// Grid: 1D, XCD-aware (xcd_remap) with the cout tile innermost, then x, y, image.
 #include "isr_common.h"
 
 namespace isr {
@@ -25,36 +27,29 @@ namespace isr {
 template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
-    static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol, unrolled chunk loop)
+    static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol)
     static constexpr int TH = R * WM;
     static constexpr int TW = 32;
     static constexpr int HR = TH + 2;  // halo rows
     static constexpr int HC = TW + 2;  // halo cols
     static constexpr int CT = NF * 32; // output channels per block
-    static constexpr int UPP = KC / 8; // 16-byte units per halo pixel
-    static constexpr int KS = KC / 16; // MFMA k-steps per chunk
-    static constexpr int HALO_UNITS = HR * HC * UPP;
-    static constexpr int HALO_INSTR = (HALO_UNITS + 63) / 64;
-    static constexpr int W_UNITS = 9 * KS * CT * 2; // [c16][tap][n][hpos] x 16 B
-    static constexpr int W_INSTR = W_UNITS / 64;
+    static constexpr int KS = KC / 16; // MFMA k-steps (= planes) per chunk
+    static constexpr int HQ = HR * HC; // halo pixels per plane
+    static constexpr int HIPL = (HQ + 31) / 32; // glds instructions per plane (32 px x 32 B each)
+    static constexpr int HALO_INSTR = KS * HIPL;
+    static constexpr int W_INSTR = 9 * KS * CT / 32; // [ks][tap][n][hpos] x 16 B
     static constexpr int INSTR = HALO_INSTR + W_INSTR;
     static constexpr int IPW = (INSTR + WM - 1) / WM; // glds per wave per chunk (uniform)
     static constexpr int STAGE = IPW * WM * 1024;
     static constexpr int NT = 64 * WM;
-    static constexpr int EPS = CT + 4;                // floats per pixel in the epilogue image
+    static constexpr int EPS = CT + 4;                 // floats per pixel in the epilogue image
     static constexpr int EP_BYTES = WM * 32 * EPS * 4; // one output row per wave at a time
     static constexpr int LDS = (NST * STAGE > EP_BYTES) ? NST * STAGE : EP_BYTES;
-    static constexpr int OCC = (163840 / LDS) * WM / 4 >= 2 ? 2 : 1; // waves per SIMD to budget registers for
-    static_assert(W_UNITS % 64 == 0, "weight stage must be whole glds instructions");
+    static constexpr int BPC = 163840 / LDS; // blocks per CU by LDS
+    static constexpr int OCC = BPC * WM / 4 >= 2 ? 2 : 1; // waves per SIMD to budget registers for
     static_assert(LDS <= 163840, "LDS budget");
     static_assert(KC == 16 || KC == 32, "chunk width");
 };
-
-__device__ __forceinline__ int swz_unit(int q, int c, int upp) {
-    // halo image: UPP units of 16 B per pixel, XOR-swizzled so that the 32
-    // consecutive pixels of an A-fragment ds_read_b128 hit 16 distinct slots.
-    return upp == 4 ? q * 4 + (c ^ ((q >> 2) & 3)) : q * 2 + (c ^ ((q >> 3) & 1));
-}
 
 // Packed weights (isr_pack_conv3x3): [c16 = cin/16][tap 9][cout][hpos 2][8 bf16],
 // element = W[n][c16*16 + h*8 + e][tap], h = hpos ^ ((n >> 3) & 1).
@@ -64,10 +59,14 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     constexpr int R = C::R, NF = C::NF, WM = C::WM;
 
     const int nct = d.cout / C::CT;
-    const int img = blockIdx.z / nct;
-    const int ct = blockIdx.z - img * nct;
-    const int x0 = blockIdx.x * C::TW;
-    const int y0 = blockIdx.y * C::TH;
+    const int nbx = d.wa / C::TW, nby = d.ha / C::TH;
+    int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int ct = t % nct; t /= nct;
+    const int bx = t % nbx; t /= nbx;
+    const int by = t % nby;
+    const int img = t / nby;
+    const int x0 = bx * C::TW;
+    const int y0 = by * C::TH;
     const int wave = wave_id();
     const int lane = threadIdx.x & 63;
     const int l31 = lane & 31;
@@ -75,29 +74,29 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     const int nchunks = C::CIN ? C::CIN / C::KC : d.cin / C::KC;
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
-    const char* xbase = view_px(d.x, img, y0 - 1, x0 - 1);
+    const char* xbase = view_at(d.x, img, y0 - 1, x0 - 1, 0);
+    const size_t pstride = plane_bytes(d.x);
     const char* wbase = (const char*)d.wpack;
-    const int xrow_bytes = d.x.wp * d.x.cs * 2;
-    const int xpix_bytes = d.x.cs * 2;
-    const int wchunk_bytes = C::KS * 9 * d.cout * 32;
+    const int xrow_bytes = d.x.wp * 32;
+    const size_t wchunk_bytes = (size_t)C::KS * 9 * d.cout * 32;
     uint32_t off[C::IPW];
 #pragma unroll
     for (int k = 0; k < C::IPW; ++k) {
         const int j = wave + WM * k;
         uint32_t o = 0;
         if (j < C::HALO_INSTR) {
-            const int u = j * 64 + lane;
-            if (u < C::HALO_UNITS) {
-                const int q = u / C::UPP;
-                const int cpos = u - q * C::UPP;
+            const int kp = j / C::HIPL;
+            const int u = (j - kp * C::HIPL) * 64 + lane;
+            const int q = u >> 1;
+            if (q < C::HQ) {
                 const int row = q / C::HC;
                 const int col = q - row * C::HC;
-                const int c = C::UPP == 4 ? (cpos ^ ((q >> 2) & 3)) : (cpos ^ ((q >> 3) & 1));
-                o = (uint32_t)(row * xrow_bytes + col * xpix_bytes + c * 16);
+                const int c = (u & 1) ^ ((q >> 3) & 1);
+                o = (uint32_t)(kp * pstride + row * xrow_bytes + col * 32 + c * 16);
             }
         } else if (j < C::INSTR) {
             const int u = (j - C::HALO_INSTR) * 64 + lane;
-            const int seg = u / (C::CT * 2); // (c16l, tap)
+            const int seg = u / (C::CT * 2); // (ks, tap)
             const int rem = u - seg * (C::CT * 2);
             o = (uint32_t)((seg * d.cout + ct * C::CT) * 32 + rem * 16);
         }
@@ -106,7 +105,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
 
     auto stage = [&](int chunk, int buf) {
         char* dst = smem + buf * C::STAGE;
-        const char* xs = xbase + chunk * (C::KC * 2);
+        const char* xs = xbase + (size_t)chunk * C::KS * pstride;
         const char* ws = wbase + (size_t)chunk * wchunk_bytes;
 #pragma unroll
         for (int k = 0; k < C::IPW; ++k) {
@@ -148,6 +147,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         const char* ws = hs + C::HALO_INSTR * 1024;
 #pragma unroll
         for (int ks = 0; ks < C::KS; ++ks) {
+            const char* hp = hs + ks * C::HIPL * 1024;
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx) {
                 bf16x8 b[3][NF];
@@ -159,11 +159,10 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
                         const int u = ((ks * 9 + dy * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
                         b[dy][f] = lds_read16(ws + u * 16);
                     }
-                const int c = 2 * ks + hh;
 #pragma unroll
                 for (int i = 0; i < R + 2; ++i) {
                     const int q = qw + i * C::HC + dx;
-                    const bf16x8 a = lds_read16(hs + swz_unit(q, c, C::UPP) * 16);
+                    const bf16x8 a = lds_read16(hp + halo_unit2(q, hh) * 16);
 #pragma unroll
                     for (int dy = 0; dy < 3; ++dy) {
                         const int r = i - dy;
@@ -220,8 +219,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
 #pragma unroll
                     for (int k = 0; k < 8; ++k) v[k] = 0.f;
                 }
-                char* dst = view_px(e.y, img, 2 * yy + si, 2 * x0 + xo) + (ct * (C::CT / 4) + cg * 8) * 2;
-                store8_bf16(dst, v);
+                store8_bf16(view_at(e.y, img, 2 * yy + si, 2 * x0 + xo, ct * (C::CT / 4) + cg * 8), v);
             }
         } else {
             constexpr int CG = C::CT / 8;
@@ -246,30 +244,32 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
 
 template <class C>
 static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
-    if (d->cout % C::CT) return -2;
-    if (d->cin % C::KC) return -2;
+    if (d->cout % C::CT || d->cin % C::KC || d->ha % C::TH) return -2;
+    if (C::CIN && d->cin != C::CIN) return -2;
     auto kern = conv3x3_fwd_kernel<C>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
         attr = true;
     }
-    dim3 grid(d->wa / C::TW, d->ha / C::TH, d->n * (d->cout / C::CT));
-    hipLaunchKernelGGL(kern, grid, dim3(C::NT), C::LDS, s, *d);
+    const int blocks = (d->wa / C::TW) * (d->ha / C::TH) * d->n * (d->cout / C::CT);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Variant table: the production choice per shape is variant 0; the others are
-// kept for on-device A/B tuning (isr_conv3x3_fwd_variant).
-using V_G0 = C3<2, 4, 1, 32, 2>;  // cout 32: TH 8, 80 KB → 2 blocks / CU (fastest, tools/tune_conv.py r1)
-using V_G1 = C3<4, 4, 1, 32, 2>;  // cout 32: 115 KB → 1 block / CU (first version)
-using V_G2 = C3<4, 4, 1, 16, 3>;  // cout 32: 3-deep ring
-using V_G3 = C3<4, 4, 1, 16, 2>;  // cout 32: 58 KB → 2 blocks / CU
-using V_W0 = C3<4, 4, 2, 16, 2>;  // cout %64: 80 KB → 2 blocks / CU (fastest, tools/tune_conv.py r1)
-using V_F0 = C3<4, 4, 2, 16, 2, 192>;  // RDB final conv 192→64: V_W0 with compile-time cin
-using V_W1 = C3<4, 4, 2, 32, 2>;  // cout %64: 150 KB → 1 block / CU (round-1 baseline)
-using V_W2 = C3<2, 4, 2, 32, 2>;  // cout %64: TH 8
-using V_W3 = C3<4, 4, 2, 16, 3>;  // cout %64: 3-deep ring, KC 16
+// Variant table: variant 0 is the production choice per shape; the others are
+// kept for on-device A/B tuning (isr_conv3x3_fwd_variant, tools/tune_conv.py).
+// cout == 32 (RDB growth convs)
+using V_G0 = C3<4, 8, 1, 16, 3>; // 32x32 px tile, 8 waves, 3-deep KC16 ring
+using V_G1 = C3<4, 4, 1, 16, 2>; // 16x32, 2 blocks / CU
+using V_G2 = C3<2, 4, 1, 32, 2>; // 8x32, KC32, 2 blocks / CU (r1 production)
+using V_G3 = C3<2, 8, 1, 16, 3>; // 16x32, 8 waves x 2 rows, 3-deep KC16 ring
+// cout % 64 == 0
+using V_W0 = C3<4, 8, 2, 16, 2>; // 32x32 px tile, 8 waves, KC16 double buffer
+using V_W1 = C3<4, 4, 2, 16, 2>; // 16x32, 2 blocks / CU (r1 production)
+using V_W2 = C3<2, 4, 2, 32, 2>; // 8x32, KC32
+using V_W3 = C3<4, 4, 2, 32, 2>; // 16x32, KC32, 1 block / CU
+using V_F0 = C3<4, 8, 2, 16, 2, 192>; // RDB final conv 192→64: V_W0 with compile-time cin
 
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
     if (d->cout == 32) {

@@ -151,16 +151,16 @@ constexpr int TH = 16, TW = 32, WM = 4;
 constexpr int TR = TH + 8;        // T rows (input rows of the tile)
 constexpr int RT = TR / WM;       // T rows per wave (6)
 constexpr int HC = TW + 8;        // 40 halo cols
-constexpr int HALO_UNITS = TR * HC * 4;       // 3840
-constexpr int HALO_INSTR = HALO_UNITS / 64;   // 60
-constexpr int HALO_BYTES = HALO_UNITS * 16;   // 61440
+constexpr int HIPL = TR * HC / 32;           // 30 glds per 16-channel plane (32 px x 32 B)
+constexpr int HALO_INSTR = 2 * HIPL;          // 60 per 32-channel chunk
+constexpr int HALO_BYTES = HALO_INSTR * 1024; // 61440
 constexpr int W_BYTES = 9 * 2 * 2 * 32 * 32;  // [kx][chunk][ks][n][hpos][8] bf16 = 36864
 constexpr int W_INSTR = W_BYTES / 1024;       // 36
 constexpr int TS = 33;                        // floats per pixel in the T image (conflict-free column sums)
 constexpr int T_BYTES = TR * 32 * TS * 4;     // 101376
 constexpr int P1 = HALO_BYTES + W_BYTES;      // 98304
 constexpr int LDS = P1 > T_BYTES ? P1 : T_BYTES;
-static_assert(HALO_UNITS % 64 == 0, "");
+static_assert(TR * HC % 32 == 0, "");
 }  // namespace tail
 
 // packed tail weights: [kx 9][chunk 2][ks 2][n 32][hpos 2][8] bf16,
@@ -173,8 +173,9 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
     const int wave = wave_id();
     const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
 
-    const char* xbase = view_px(d.x, img, y0 - 4, x0 - 4);
-    const int xrow = d.x.wp * d.x.cs * 2, xpix = d.x.cs * 2;
+    const char* xbase = view_at(d.x, img, y0 - 4, x0 - 4, 0);
+    const size_t pstride = plane_bytes(d.x);
+    const int xrow = d.x.wp * 32;
     char* halo = smem;
     char* wl = smem + HALO_BYTES;
 
@@ -190,12 +191,14 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
             for (int j = wave; j < W_INSTR; j += WM)
                 glds16((const char*)d.wpack + j * 1024 + lane * 16, wl + j * 1024);
         }
+        // halo image [plane kp][pixel q][2 units], 32 pixels of one plane per glds
         for (int j = wave; j < HALO_INSTR; j += WM) {
-            const int u = j * 64 + lane;
-            const int q = u >> 2, cpos = u & 3;
+            const int kp = j / HIPL;
+            const int u = (j - kp * HIPL) * 64 + lane;
+            const int q = u >> 1;
             const int row = q / HC, col = q - row * HC;
-            const int c = cpos ^ ((q >> 2) & 3);
-            glds16(xbase + row * xrow + col * xpix + chunk * 64 + c * 16, halo + j * 1024);
+            const int c = (u & 1) ^ ((q >> 3) & 1);
+            glds16(xbase + (size_t)(chunk * 2 + kp) * pstride + row * xrow + col * 32 + c * 16, halo + j * 1024);
         }
         wait_vm0();
         __syncthreads();
@@ -205,11 +208,11 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
             for (int ks = 0; ks < 2; ++ks) {
                 const int n = l31;
                 const bf16x8 b = lds_read16(wl + ((((kx * 2 + chunk) * 2 + ks) * 32 + n) * 2 + (hh ^ ((n >> 3) & 1))) * 16);
-                const int c = 2 * ks + hh;
+                const char* hp = halo + ks * HIPL * 1024;
 #pragma unroll
                 for (int t = 0; t < RT; ++t) {
                     const int q = (wave * RT + t) * HC + kx + l31;
-                    acc[t] = mfma32(lds_read16(halo + halo_unit(q, c) * 16), b, acc[t]);
+                    acc[t] = mfma32(lds_read16(hp + halo_unit2(q, hh) * 16), b, acc[t]);
                 }
             }
         }

@@ -37,16 +37,32 @@ __device__ __forceinline__ int wave_id() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
-// Byte address of interior pixel (img, y, x), channel 0 of a view.
-__device__ __forceinline__ char* view_px(const isr_view& v, int img, int y, int x) {
-    size_t pix = ((size_t)img * v.hp + (y + v.pad)) * (size_t)v.wp + (size_t)(x + v.pad);
-    return (char*)v.data + (pix * (size_t)v.cs + (size_t)v.coff) * 2;
+// Activations are channel-blocked: [N][cs/16][hp][wp][16] bf16 (one 16-channel
+// "plane" per block of channels).  Byte address of interior pixel (img, y, x),
+// view channel c (c % 8 == 0 for vector accesses).
+__device__ __forceinline__ char* view_at(const isr_view& v, int img, int y, int x, int c) {
+    const int ch = v.coff + c;
+    const size_t plane = (size_t)img * (v.cs >> 4) + (ch >> 4);
+    const size_t pix = (plane * v.hp + (y + v.pad)) * (size_t)v.wp + (size_t)(x + v.pad);
+    return (char*)v.data + (pix * 16 + (ch & 15)) * 2;
 }
 
-// Swizzled position of 16-byte unit (pixel q, channel-chunk c in 0..3) in an
-// LDS halo image with 64 B per pixel.  XOR with bits 2..3 of q makes the
-// 32-consecutive-pixel ds_read_b128 of an MFMA A fragment bank-conflict free.
-__device__ __forceinline__ int halo_unit(int q, int c) { return q * 4 + (c ^ ((q >> 2) & 3)); }
+// Byte stride between consecutive 16-channel planes of a view.
+__device__ __forceinline__ size_t plane_bytes(const isr_view& v) { return (size_t)v.hp * v.wp * 32; }
+
+// Bijective XCD-aware remap of a 1D block id: blocks b and b+8 run on the same
+// XCD (round-robin dispatch, MI355X_MICROARCH.md), so give each XCD a
+// contiguous range of logical tiles — neighbouring tiles share halo rows in
+// that XCD's L2.  Speed only; any placement is correct.
+__device__ __forceinline__ int xcd_remap(int b, int total) {
+    const int q = total >> 3, r = total & 7, x = b & 7, k = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+// LDS halo plane image: 2 units of 16 B (8 channels) per pixel, XOR-swizzled
+// by bit 3 of the pixel index so that the 32 consecutive pixels of an MFMA A
+// fragment (one ds_read_b128 per lane) hit 16 distinct bank slots per lane group.
+__device__ __forceinline__ int halo_unit2(int q, int c) { return q * 2 + (c ^ ((q >> 3) & 1)); }
 
 __device__ __forceinline__ void load8_bf16(const char* p, float* v) {
     bf16x8 t = *reinterpret_cast<const bf16x8*>(p);
@@ -82,13 +98,13 @@ __device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int 
     const bool valid = (yy < e.h) && (xx < e.w);
     if (e.r1.data) {
         float r[8];
-        load8_bf16(view_px(e.r1, img, yy, xx) + co * 2, r);
+        load8_bf16(view_at(e.r1, img, yy, xx, co), r);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = v[k] * e.s1 + r[k];
     }
     if (e.r2.data) {
         float r[8];
-        load8_bf16(view_px(e.r2, img, yy, xx) + co * 2, r);
+        load8_bf16(view_at(e.r2, img, yy, xx, co), r);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = v[k] * e.s2 + r[k];
     }
@@ -96,8 +112,8 @@ __device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int 
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = 0.f;
     }
-    store8_bf16(view_px(e.y, img, yy, xx) + co * 2, v);
-    if (e.y2.data) store8_bf16(view_px(e.y2, img, yy, xx) + co * 2, v);
+    store8_bf16(view_at(e.y, img, yy, xx, co), v);
+    if (e.y2.data) store8_bf16(view_at(e.y2, img, yy, xx, co), v);
 }
 
 }  // namespace isr

@@ -31,11 +31,12 @@ def _require_gpu(t: torch.Tensor, what: str) -> None:
 
 @dataclass
 class ActBuffer:
-    """NHWC bf16 activation buffer [n][ha+2p][wa+2p][c] with a zero border of p pixels.
+    """Channel-blocked bf16 activation buffer [n][c/16][ha+2p][wa+2p][16], zero border p.
 
-    (h, w) is the valid image size, (ha, wa) the tile-aligned computed extent.
-    Kernels keep every position outside (h, w) at exactly zero, so the border
-    and alignment slack act as the convolution's zero padding.
+    Each 16-channel block is a contiguous plane, so a conv K-chunk reads whole
+    cache lines.  (h, w) is the valid image size, (ha, wa) the tile-aligned
+    computed extent.  Kernels keep every position outside (h, w) at exactly
+    zero, so the border and alignment slack act as the conv's zero padding.
     """
     t: torch.Tensor
     n: int
@@ -48,32 +49,52 @@ class ActBuffer:
     @staticmethod
     def alloc(n: int, h: int, w: int, c: int, pad: int, device, ha: int | None = None,
               wa: int | None = None) -> "ActBuffer":
+        if c % 16:
+            raise ValueError(f"ActBuffer channels must be a multiple of 16, got {c}")
         ha = round_up(h, TILE_H) if ha is None else ha
         wa = round_up(w, TILE_W) if wa is None else wa
-        t = torch.zeros((n, ha + 2 * pad, wa + 2 * pad, c), dtype=torch.bfloat16, device=device)
+        t = torch.zeros((n, c // 16, ha + 2 * pad, wa + 2 * pad, 16), dtype=torch.bfloat16, device=device)
         return ActBuffer(t, n, h, w, ha, wa, pad)
 
     @property
     def c(self) -> int:
-        return self.t.shape[3]
+        return self.t.shape[1] * 16
 
     def view(self, coff: int = 0) -> IsrView:
-        return IsrView(self.t.data_ptr(), self.t.shape[1], self.t.shape[2], self.t.shape[3], self.pad, coff)
+        return IsrView(self.t.data_ptr(), self.t.shape[2], self.t.shape[3], self.c, self.pad, coff)
 
     def interior(self, c0: int = 0, c1: int | None = None) -> torch.Tensor:
-        """Valid region as a [n, h, w, c] view (for tests / debugging)."""
+        """Valid region as an [n, c, h, w] strided view (for tests / debugging)."""
         p = self.pad
-        return self.t[:, p:p + self.h, p:p + self.w, c0:c1]
+        v = self.t[:, :, p:p + self.h, p:p + self.w, :]  # n, c16, h, w, 16
+        v = v.permute(0, 1, 4, 2, 3).reshape(self.n, self.c, self.h, self.w)
+        return v[:, c0:c1]
+
+    def set_nchw(self, x: torch.Tensor, c0: int = 0) -> None:
+        """Write NCHW x into channels [c0, c0 + x.shape[1]) of the valid region."""
+        n, c, h, w = x.shape
+        if c % 16 or c0 % 16 or (h, w) != (self.h, self.w):
+            raise ValueError("set_nchw: channel block / shape mismatch")
+        p = self.pad
+        self.t[:, c0 // 16:(c0 + c) // 16, p:p + h, p:p + w, :] = (
+            x.reshape(n, c // 16, 16, h, w).permute(0, 1, 3, 4, 2).to(torch.bfloat16))
+
+    def outside_valid(self) -> torch.Tensor:
+        """Every element outside the valid h x w region (border + alignment slack)."""
+        mask = torch.ones(self.t.shape, dtype=torch.bool, device=self.t.device)
+        p = self.pad
+        mask[:, :, p:p + self.h, p:p + self.w, :] = False
+        return self.t[mask]
 
     @staticmethod
     def from_nchw(x: torch.Tensor, pad: int = 1, c_alloc: int | None = None) -> "ActBuffer":
         n, c, h, w = x.shape
         buf = ActBuffer.alloc(n, h, w, c_alloc or c, pad, x.device)
-        buf.t[:, pad:pad + h, pad:pad + w, :c] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+        buf.set_nchw(x, 0)
         return buf
 
     def to_nchw(self, c0: int = 0, c1: int | None = None) -> torch.Tensor:
-        return self.interior(c0, c1).permute(0, 3, 1, 2).float()
+        return self.interior(c0, c1).float().contiguous()
 
 
 _NULL_VIEW = IsrView(None, 0, 0, 0, 0, 0)

@@ -9,11 +9,13 @@
  * INTEGRATION.md); no torch types cross this boundary.
  *
  * Conventions
- *  - Activations are NHWC bf16 in caller-owned device buffers laid out as
- *    [N][hp][wp][cs] with a zero border of `pad` pixels on every side.  The
- *    caller zero-fills a buffer once; kernels never write the border and write
- *    exact zeros at computed positions outside the valid h x w region, so the
- *    border / alignment slack always reads as the conv's zero padding.
+ *  - Activations are channel-blocked bf16 ("NC16HW16c") in caller-owned device
+ *    buffers laid out as [N][cs/16][hp][wp][16] with a zero border of `pad`
+ *    pixels on every side: each 16-channel block is a contiguous plane, so a
+ *    K-chunk of a convolution reads whole cache lines.  The caller zero-fills a
+ *    buffer once; kernels never write the border and write exact zeros at
+ *    computed positions outside the valid h x w region, so the border /
+ *    alignment slack always reads as the conv's zero padding.
  *  - Computed regions are tile-aligned: ha % ISR_TILE_H == 0, wa % ISR_TILE_W == 0.
  *  - The library never allocates, frees or synchronises; every call takes an
  *    explicit stream and is hipGraph-capturable.
@@ -37,12 +39,13 @@ typedef struct ihipStream_t* isr_stream_t; /* == hipStream_t */
 #define ISR_ERR_UNSUPPORTED (-2)
 #define ISR_ERR_LAUNCH (-3)
 
-#define ISR_TILE_H 16
+#define ISR_TILE_H 32
 #define ISR_TILE_W 32
 
-/* A channel slice of an NHWC bf16 buffer [N][hp][wp][cs] with border `pad`.
- * Interior pixel (n, y, x), channel c lives at
- *   data + (((n*hp + y + pad) * wp + x + pad) * cs + coff + c) * 2 bytes. */
+/* A channel slice [coff, coff + k) of a channel-blocked bf16 buffer
+ * [N][cs/16][hp][wp][16] with border `pad` (cs, coff multiples of 16).
+ * Interior pixel (n, y, x), view channel c (ch = coff + c) lives at
+ *   data + ((((n*(cs/16) + ch/16)*hp + y + pad)*wp + x + pad)*16 + ch%16) * 2 bytes. */
 typedef struct isr_view {
     void* data;
     int32_t hp, wp, cs, pad, coff;
@@ -60,7 +63,7 @@ typedef struct isr_view {
  * PixelShuffle(2) → LeakyReLU via shuffle == 2). */
 typedef struct isr_conv_desc {
     int32_t n, h, w;   /* batch; valid conv height/width (input == output size) */
-    int32_t ha, wa;    /* computed (tile-aligned) extent; ha % 16 == 0, wa % 32 == 0 */
+    int32_t ha, wa;    /* computed (tile-aligned) extent; ha % 32 == 0, wa % 32 == 0 */
     int32_t cin, cout; /* cin % 32 == 0; cout == 32 or cout % 64 == 0 */
     isr_view x;        /* input (cin channels from x.coff) */
     isr_view y;        /* output; for shuffle == 2 its grid is (2h, 2w), cout/4 channels */

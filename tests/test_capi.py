@@ -72,13 +72,13 @@ def test_validation_rejects_without_touching_gpu(built_lib):
     assert lib.isr_conv3x3_fwd(None, None) == -1
     assert b"null descriptor" in lib.isr_last_error()
     d = _lib.IsrConvDesc()
-    d.n, d.h, d.w, d.ha, d.wa, d.cin, d.cout = 1, 16, 32, 16, 32, 48, 64
+    d.n, d.h, d.w, d.ha, d.wa, d.cin, d.cout = 1, 16, 32, 32, 32, 48, 64
     assert lib.isr_conv3x3_fwd(ctypes.byref(d), None) == -2
     assert b"multiple of 32" in lib.isr_last_error()
     d.cin = 64
-    d.ha = 8  # not tile aligned
+    d.ha = 16  # not tile aligned (ISR_TILE_H = 32)
     assert lib.isr_conv3x3_fwd(ctypes.byref(d), None) == -1
-    d.ha = 16
+    d.ha = 32
     assert lib.isr_conv3x3_fwd(ctypes.byref(d), None) == -1  # null weights / views
     assert lib.isr_head9x9_fwd(None, None) == -1
     assert lib.isr_tail9x9_fwd(None, None) == -1

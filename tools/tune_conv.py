@@ -43,7 +43,7 @@ def main():
     for cin, cout, shuffle, s in shapes:
         g = torch.Generator().manual_seed(cin + cout)
         src = ops.ActBuffer.alloc(n, s, s, 192, 1, dev)
-        src.t[:, 1:1 + s, 1:1 + s, :cin] = torch.randn(n, s, s, cin, generator=g).to(dev, torch.bfloat16)
+        src.set_nchw(torch.randn(n, cin, s, s, generator=g).to(dev), 0)
         w = (torch.rand(cout, cin, 3, 3, generator=g) * 2 - 1).mul((3.0 / (cin * 9)) ** 0.5).to(dev)
         b = torch.randn(cout, generator=g).mul(0.1).to(dev)
         wp = ops.pack_conv3x3(w)
@@ -65,7 +65,7 @@ def main():
             if rc == 0:
                 ok.append(v)
                 torch.cuda.synchronize()
-                sl = dst.t[..., cin:cin + 32] if (cout == 32) else dst.t
+                sl = dst.t[:, cin // 16:cin // 16 + 2] if (cout == 32) else dst.t
                 outs[v] = sl.float().clone()
         times = {v: [] for v in ok}
         for _ in range(args.rounds):
