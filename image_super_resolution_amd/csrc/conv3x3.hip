@@ -24,10 +24,14 @@
 
 namespace isr {
 
-template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0>
+template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1)>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
+    static constexpr int PIPE = PIPE_; // 1: double-buffered fragment registers across (k-step, dx) steps
     static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol)
+    // Ablation bits, timing-only builds (outputs wrong): 1 = no MFMA (operands
+    // kept live), 2 = stage only chunk 0 (no refill), 4 = no epilogue stores.
+    static constexpr int ABL = ABL_;
     static constexpr int TH = R * WM;
     static constexpr int TW = 32;
     static constexpr int HR = TH + 2;  // halo rows
@@ -50,6 +54,111 @@ struct C3 {
     static_assert(LDS <= 163840, "LDS budget");
     static_assert(KC == 16 || KC == 32, "chunk width");
 };
+
+__device__ __forceinline__ void swap_halves(float& lo, float& hi) {
+    // v_permlane32_swap: lanes 32..63 of `lo` trade places with lanes 0..31 of `hi`
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+    lo = __uint_as_float(r[0]);
+    hi = __uint_as_float(r[1]);
+}
+
+// Epilogue.  Accumulators are D[cout][pixel]: lane l owns pixel l31 of the row
+// and couts (g&3) + 8*(g>>2) + 4*hh of each 32-cout fragment; the bias is
+// already in them (accumulator init).
+//  * plain stores (MODE 0..7): two v_permlane32_swap rounds per fragment give
+//    every lane 8 contiguous couts twice, so each store is 16 bytes and one
+//    store instruction covers 32 pixels x 32 contiguous bytes; no LDS, no
+//    barrier.  All residual loads of a row are issued before its stores (the
+//    output may alias a residual: the in-place RRDB update).
+//  * PixelShuffle(2) (MODE 8): transpose through LDS one row at a time, so a
+//    lane stores 8 channels of one shuffled output pixel.
+// MODE bits (compile-time: no per-element branches): 1 = r1, 2 = r2, 4 = y2, 8 = shuffle.
+template <class C, int MODE>
+__device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C::R][C::NF], int img, int ct,
+                                         int x0, int y0, int wave, int lane) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int R = C::R, NF = C::NF, CT = C::CT, EPS = C::EPS;
+    const int l31 = lane & 31, hh = lane >> 5;
+    const float slope = d.slope;
+    if constexpr (MODE & 8) {
+        constexpr int ITEMS = CT / 16; // items (8 channels of one shuffled pixel) per lane per row
+        constexpr int CG = CT / 32;
+        float* ep = reinterpret_cast<float*>(smem) + wave * (32 * EPS);
+        const int cg = lane % CG;
+        const int sj = (lane / CG) & 1;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int g = 0; g < 16; ++g)
+                    ep[l31 * EPS + f * 32 + (g & 3) + 8 * (g >> 2) + 4 * hh] = acc[r][f][g];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            const int yy = y0 + wave * R + r;
+#pragma unroll
+            for (int it = 0; it < ITEMS; ++it) {
+                // item → sub-row si (compile-time), output column xo, channel group cg
+                const int si = it / CG;
+                const int xo = (lane / CG + 64 * it / CG) & 63;
+                const int xc = xo >> 1;
+                float v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    v[k] = ep[xc * EPS + 4 * (cg * 8 + k) + 2 * si + sj];
+                    v[k] = v[k] >= 0.f ? v[k] : v[k] * slope;
+                }
+                if (!(yy < d.h && x0 + xc < d.w)) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) v[k] = 0.f;
+                }
+                store8_bf16(view_at(d.y, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8), v);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        }
+    } else {
+        const int xx = x0 + l31;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int yy = y0 + wave * R + r;
+            const bool valid = yy < d.h && xx < d.w;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                bf16x8 q1[2], q2[2]; // residuals of this fragment, loaded before its stores
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    const int co = ct * CT + f * 32 + 16 * blk + 8 * hh;
+                    if constexpr (MODE & 1) q1[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r1, img, yy, xx, co));
+                    if constexpr (MODE & 2) q2[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r2, img, yy, xx, co));
+                }
+                float v[16];
+#pragma unroll
+                for (int g = 0; g < 16; ++g) v[g] = acc[r][f][g];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    swap_halves(v[k], v[4 + k]);
+                    swap_halves(v[8 + k], v[12 + k]);
+                }
+                // v[8*blk + e] = cout f*32 + 16*blk + 8*hh + e
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    float* u = v + 8 * blk;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
+                        if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (float)q1[blk][e];
+                        if constexpr (MODE & 2) u[e] = u[e] * d.s2 + (float)q2[blk][e];
+                        if (!valid) u[e] = 0.f;
+                    }
+                    const int co = ct * CT + f * 32 + 16 * blk + 8 * hh;
+                    store8_bf16(view_at(d.y, img, yy, xx, co), u);
+                    if constexpr (MODE & 4) store8_bf16(view_at(d.y2, img, yy, xx, co), u);
+                }
+            }
+        }
+    }
+}
 
 // Packed weights (isr_pack_conv3x3): [c16 = cin/16][tap 9][cout][hpos 2][8 bf16],
 // element = W[n][c16*16 + h*8 + e][tap], h = hpos ^ ((n >> 3) & 1).
@@ -115,13 +224,18 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         }
     };
 
+    // D[cout][pixel] accumulators (A = weights, B = pixels): register g of lane l
+    // holds cout f*32 + (g&3) + 8*(g>>2) + 4*hh of pixel l31; the bias is the init.
     f32x16 acc[R][NF];
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int f = 0; f < NF; ++f) {
+        f32x16 b0;
 #pragma unroll
-        for (int f = 0; f < NF; ++f)
+        for (int g = 0; g < 16; ++g)
+            b0[g] = d.bias ? d.bias[ct * C::CT + f * 32 + (g & 3) + 8 * (g >> 2) + 4 * hh] : 0.f;
 #pragma unroll
-            for (int g = 0; g < 16; ++g) acc[r][f][g] = 0.f;
+        for (int r = 0; r < R; ++r) acc[r][f] = b0;
+    }
 
 #pragma unroll
     for (int s = 0; s < C::NST - 1; ++s)
@@ -141,34 +255,57 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (chunk + C::NST - 1 < nchunks) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+        if (!(C::ABL & 2) && chunk + C::NST - 1 < nchunks) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
 
-        const char* hs = smem + (chunk % C::NST) * C::STAGE;
+        const char* hs = smem + ((C::ABL & 2) ? 0 : (chunk % C::NST)) * C::STAGE;
         const char* ws = hs + C::HALO_INSTR * 1024;
-#pragma unroll
-        for (int ks = 0; ks < C::KS; ++ks) {
+        // Software pipeline over the chunk's (k-step, dx) steps: the fragments of
+        // step st+1 are read into the other register set while step st's MFMAs
+        // run, so LDS latency is covered by MFMA work of the same wave.
+        constexpr int NS = C::KS * 3;
+        bf16x8 fb[2][3][NF], fa[2][R + 2];
+        auto load_step = [&](int st, int set) {
+            const int ks = st / 3, dx = st - 3 * (st / 3);
             const char* hp = hs + ks * C::HIPL * 1024;
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx) {
-                bf16x8 b[3][NF];
+            for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-                for (int dy = 0; dy < 3; ++dy)
+                for (int f = 0; f < NF; ++f) {
+                    const int n = f * 32 + l31;
+                    const int u = ((ks * 9 + dy * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
+                    fb[set][dy][f] = lds_read16(ws + u * 16);
+                }
 #pragma unroll
-                    for (int f = 0; f < NF; ++f) {
-                        const int n = f * 32 + l31;
-                        const int u = ((ks * 9 + dy * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
-                        b[dy][f] = lds_read16(ws + u * 16);
-                    }
+            for (int i = 0; i < R + 2; ++i) {
+                const int q = qw + i * C::HC + dx;
+                fa[set][i] = lds_read16(hp + halo_unit2(q, hh) * 16);
+            }
+        };
+        if constexpr (C::PIPE) load_step(0, 0);
 #pragma unroll
-                for (int i = 0; i < R + 2; ++i) {
-                    const int q = qw + i * C::HC + dx;
-                    const bf16x8 a = lds_read16(hp + halo_unit2(q, hh) * 16);
+        for (int st = 0; st < NS; ++st) {
+            const int cur = C::PIPE ? (st & 1) : 0;
+            if constexpr (C::PIPE) {
+                if (st + 1 < NS) load_step(st + 1, cur ^ 1);
+                // keep the prefetch ahead of this step's MFMAs (hipcc otherwise sinks
+                // each ds_read next to its first use and waits lgkmcnt(0) there)
+                __builtin_amdgcn_sched_barrier(0);
+            } else {
+                load_step(st, 0);
+            }
 #pragma unroll
-                    for (int dy = 0; dy < 3; ++dy) {
-                        const int r = i - dy;
-                        if (r >= 0 && r < R) {
+            for (int i = 0; i < R + 2; ++i) {
 #pragma unroll
-                            for (int f = 0; f < NF; ++f) acc[r][f] = mfma32(a, b[dy][f], acc[r][f]);
+                for (int dy = 0; dy < 3; ++dy) {
+                    const int r = i - dy;
+                    if (r >= 0 && r < R) {
+#pragma unroll
+                        for (int f = 0; f < NF; ++f) {
+                            if constexpr (C::ABL & 1) {
+                                asm volatile("" ::"v"(fa[cur][i]), "v"(fb[cur][dy][f]));
+                            } else {
+                                acc[r][f] = mfma32(fb[cur][dy][f], fa[cur][i], acc[r][f]);
+                            }
                         }
                     }
                 }
@@ -178,67 +315,31 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier(); // all waves done reading the ring before it becomes the epilogue image
 
-    // ---- epilogue, one output row per pass: acc → LDS [px][CT] fp32 → 8-channel stores
-    float* ep = reinterpret_cast<float*>(smem) + wave * (32 * C::EPS);
-    Epi e;
-    e.bias = d.bias; e.slope = d.slope; e.s1 = d.s1; e.s2 = d.s2;
-    e.y = d.y; e.y2 = d.y2; e.r1 = d.r1; e.r2 = d.r2; e.h = d.h; e.w = d.w;
-    constexpr int ITEMS = C::CT / 16; // per lane per row
+    if constexpr (C::ABL & 4) {
+        if (d.n < 0) { // never true: keeps the accumulators (and so the MFMAs) live
+            float s = 0.f;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+            for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int f = 0; f < NF; ++f)
+                for (int f = 0; f < NF; ++f)
 #pragma unroll
-            for (int g = 0; g < 16; ++g) {
-                const int px = (g & 3) + 8 * (g >> 2) + 4 * hh;
-                ep[px * C::EPS + f * 32 + l31] = acc[r][f][g];
-            }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        const int yy = y0 + wave * R + r;
-        if (d.shuffle == 2) {
-            // item → (sub-row si, output col xo in [0,64), 8-channel group cg)
-            constexpr int CG = C::CT / 32;
-#pragma unroll
-            for (int it = 0; it < ITEMS; ++it) {
-                const int jj = lane + 64 * it;
-                const int cg = jj % CG;
-                const int rem = jj / CG;
-                const int xo = rem & 63;
-                const int si = rem >> 6;
-                const int xc = xo >> 1, sj = xo & 1;
-                const int xx = x0 + xc;
-                float v[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int col = 4 * (cg * 8 + k) + 2 * si + sj;
-                    v[k] = ep[xc * C::EPS + col] + (e.bias ? e.bias[ct * C::CT + col] : 0.f);
-                    v[k] = v[k] >= 0.f ? v[k] : v[k] * e.slope;
-                }
-                if (!(yy < e.h && xx < e.w)) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) v[k] = 0.f;
-                }
-                store8_bf16(view_at(e.y, img, 2 * yy + si, 2 * x0 + xo, ct * (C::CT / 4) + cg * 8), v);
-            }
-        } else {
-            constexpr int CG = C::CT / 8;
-#pragma unroll
-            for (int it = 0; it < ITEMS; ++it) {
-                const int jj = lane + 64 * it;
-                const int cg = jj % CG;
-                const int px = jj / CG;
-                float v[8];
-                const float* src = ep + px * C::EPS + cg * 8;
-                f32x4 a0 = *reinterpret_cast<const f32x4*>(src);
-                f32x4 a1 = *reinterpret_cast<const f32x4*>(src + 4);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) { v[k] = a0[k]; v[4 + k] = a1[k]; }
-                epi_plain8(e, v, img, yy, x0 + px, ct * C::CT + cg * 8);
-            }
+                    for (int g = 0; g < 16; ++g) s += acc[r][f][g];
+            ((float*)d.y.data)[threadIdx.x] = s;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
+        return;
+    }
+    // ---- epilogue (mode picked once, wave-uniform, so no per-element branches)
+    const int mode = d.shuffle == 2 ? 8 : ((d.r1.data ? 1 : 0) | (d.r2.data ? 2 : 0) | (d.y2.data ? 4 : 0));
+    switch (mode) {
+        case 0: epilogue<C, 0>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 1: epilogue<C, 1>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 2: epilogue<C, 2>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 3: epilogue<C, 3>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 4: epilogue<C, 4>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 5: epilogue<C, 5>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 6: epilogue<C, 6>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 7: epilogue<C, 7>(d, acc, img, ct, x0, y0, wave, lane); break;
+        default: epilogue<C, 8>(d, acc, img, ct, x0, y0, wave, lane); break;
     }
 }
 
@@ -259,17 +360,19 @@ static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
 
 // Variant table: variant 0 is the production choice per shape; the others are
 // kept for on-device A/B tuning (isr_conv3x3_fwd_variant, tools/tune_conv.py).
+// (tools/tune_conv.py on MI355X, N=16 128²: the 16x32-tile, 2-blocks/CU configs are
+// fastest on every shape of the generator; the 32x32 8-wave tiles win only at long K)
 // cout == 32 (RDB growth convs)
-using V_G0 = C3<4, 8, 1, 16, 3>; // 32x32 px tile, 8 waves, 3-deep KC16 ring
-using V_G1 = C3<4, 4, 1, 16, 2>; // 16x32, 2 blocks / CU
-using V_G2 = C3<2, 4, 1, 32, 2>; // 8x32, KC32, 2 blocks / CU (r1 production)
+using V_G0 = C3<4, 4, 1, 16, 2>; // 16x32, 4 waves, KC16 double buffer, 64 KB → 2 blocks / CU
+using V_G1 = C3<4, 8, 1, 16, 3>; // 32x32 px tile, 8 waves, 3-deep KC16 ring
+using V_G2 = C3<2, 4, 1, 32, 2>; // 8x32, KC32, 2 blocks / CU
 using V_G3 = C3<2, 8, 1, 16, 3>; // 16x32, 8 waves x 2 rows, 3-deep KC16 ring
 // cout % 64 == 0
-using V_W0 = C3<4, 8, 2, 16, 2>; // 32x32 px tile, 8 waves, KC16 double buffer
-using V_W1 = C3<4, 4, 2, 16, 2>; // 16x32, 2 blocks / CU (r1 production)
+using V_W0 = C3<4, 4, 2, 16, 2>; // 16x32, 4 waves, KC16 double buffer, 80 KB → 2 blocks / CU
+using V_W1 = C3<4, 8, 2, 16, 2>; // 32x32 px tile, 8 waves, KC16 double buffer
 using V_W2 = C3<2, 4, 2, 32, 2>; // 8x32, KC32
 using V_W3 = C3<4, 4, 2, 32, 2>; // 16x32, KC32, 1 block / CU
-using V_F0 = C3<4, 8, 2, 16, 2, 192>; // RDB final conv 192→64: V_W0 with compile-time cin
+using V_F0 = C3<4, 4, 2, 16, 2, 192>; // RDB final conv 192→64: V_W0 with compile-time cin
 
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
     if (d->cout == 32) {
@@ -278,6 +381,11 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 1: return launch3x3<V_G1>(d, s);
             case 2: return launch3x3<V_G2>(d, s);
             case 3: return launch3x3<V_G3>(d, s);
+            // ablations of V_G1 (timing only)
+            case 4: return launch3x3<C3<4, 4, 1, 16, 2, 0, 1>>(d, s);
+            case 5: return launch3x3<C3<4, 4, 1, 16, 2, 0, 2>>(d, s);
+            case 6: return launch3x3<C3<4, 4, 1, 16, 2, 0, 4>>(d, s);
+            case 7: return launch3x3<C3<4, 4, 1, 16, 2, 0, 3>>(d, s);
         }
         return -2;
     }
@@ -286,6 +394,11 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
         case 1: return launch3x3<V_W1>(d, s);
         case 2: return launch3x3<V_W2>(d, s);
         case 3: return launch3x3<V_W3>(d, s);
+        // ablations of V_W0 (timing only)
+        case 4: return launch3x3<C3<4, 4, 2, 16, 2, 0, 1>>(d, s);
+        case 5: return launch3x3<C3<4, 4, 2, 16, 2, 0, 2>>(d, s);
+        case 6: return launch3x3<C3<4, 4, 2, 16, 2, 0, 4>>(d, s);
+        case 7: return launch3x3<C3<4, 4, 2, 16, 2, 0, 3>>(d, s);
     }
     return -2;
 }

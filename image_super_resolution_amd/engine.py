@@ -147,7 +147,9 @@ class GeneratorPlan:
     """
 
     def __init__(self, gw: GeneratorWeights, n: int, h: int, w: int, device, x_u8: bool, out_u8: bool,
-                 mean, std):
+                 mean, std, variants: dict | None = None):
+        """`variants` (tuning only) maps ("conv3x3", cin, cout) or ("conv3x3", "*", cout)
+        to an isr_conv3x3_fwd_variant id; unlisted convs use the production kernel."""
         self.key = (n, h, w, str(device), x_u8, out_u8, tuple(mean), tuple(std))
         bufs = GeneratorBuffers(n, h, w, len(gw.scalers), device)
         self.bufs = bufs
@@ -162,11 +164,13 @@ class GeneratorPlan:
         dummy_out = torch.empty(self.out_shape, dtype=self.out_dtype, device=device)
         self.head_desc = ops.head9x9_desc(dummy_x, gw.head.w, gw.head.b, feat, slope=gw.conv0_slope, y2=X,
                                           mean=mean, std=std)
-        L = [(head, self.head_desc, ("head9x9", 3, 64))]
+        L = [(head, self.head_desc, ("head9x9", 3, 64), None)]
+        self._conv_variant = lib.isr_conv3x3_fwd_variant
 
         def c3(src, pc, dst, **kw):
-            L.append((conv, ops.conv3x3_desc(src, pc.cin, pc.w, pc.b, pc.cout, dst, **kw),
-                      ("conv3x3", pc.cin, pc.cout)))
+            tag = ("conv3x3", pc.cin, pc.cout)
+            v = (variants or {}).get(tag, (variants or {}).get(("conv3x3", "*", pc.cout)))
+            L.append((conv, ops.conv3x3_desc(src, pc.cin, pc.w, pc.b, pc.cout, dst, **kw), tag, v))
 
         ar = gw.add_rate
         for blk in gw.rdb:
@@ -181,7 +185,7 @@ class GeneratorPlan:
             c3(cur, pc, bufs.up[s], slope=LEAKY_DEFAULT, shuffle=2)
             cur = bufs.up[s]
         self.tail_desc = ops.tail9x9_desc(cur, gw.tail.w, gw.tail.b, dummy_out)
-        L.append((tail, self.tail_desc, ("tail9x9", 64, 3)))
+        L.append((tail, self.tail_desc, ("tail9x9", 64, 3), None))
         self.launches = L
         self._keep = (dummy_x, dummy_out)
 
@@ -196,11 +200,12 @@ class GeneratorPlan:
         self.tail_desc.y = out.data_ptr()
         stream = ops._stream()
         byref = ctypes.byref
-        for fn, d, tag in self.launches:
+        cv = self._conv_variant
+        for fn, d, tag, var in self.launches:
             ev = around(tag) if around is not None else None
             if ev is not None:
                 ev[0].record()
-            rc = fn(byref(d), stream)
+            rc = fn(byref(d), stream) if var is None else cv(byref(d), var, stream)
             if rc != 0:
                 ops.check(rc, f"{tag[0]} launch")
             if ev is not None:

@@ -35,14 +35,16 @@ def main():
     n, hw = args.n, args.hw
     variants = [int(v) for v in args.variants.split(",")]
     shapes = [(64, 32, 1, hw), (96, 32, 1, hw), (128, 32, 1, hw), (160, 32, 1, hw), (192, 64, 1, hw),
-              (64, 64, 1, hw), (64, 256, 2, hw), (64, 256, 2, 2 * hw)]
+              (64, 64, 1, hw), (64, 256, 2, hw), (64, 256, 2, 2 * hw),
+              # long-K shapes: fixed per-block latency amortised → main-loop throughput
+              (512, 32, 1, hw), (512, 64, 1, hw)]
     if args.only:
         keep = {tuple(int(v) for v in s.split("x")) for s in args.only.split(",")}
         shapes = [s for s in shapes if (s[0], s[1]) in keep]
     results = []
     for cin, cout, shuffle, s in shapes:
         g = torch.Generator().manual_seed(cin + cout)
-        src = ops.ActBuffer.alloc(n, s, s, 192, 1, dev)
+        src = ops.ActBuffer.alloc(n, s, s, max(192, cin + 32), 1, dev)
         src.set_nchw(torch.randn(n, cin, s, s, generator=g).to(dev), 0)
         w = (torch.rand(cout, cin, 3, 3, generator=g) * 2 - 1).mul((3.0 / (cin * 9)) ** 0.5).to(dev)
         b = torch.randn(cout, generator=g).mul(0.1).to(dev)
