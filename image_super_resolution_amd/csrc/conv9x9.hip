@@ -158,8 +158,10 @@ constexpr int W_BYTES = 9 * 2 * 2 * 32 * 32;  // [kx][chunk][ks][n][hpos][8] bf1
 constexpr int W_INSTR = W_BYTES / 1024;       // 36
 constexpr int TS = 33;                        // floats per pixel in the T image (conflict-free column sums)
 constexpr int T_BYTES = TR * 32 * TS * 4;     // 101376
-constexpr int P1 = HALO_BYTES + W_BYTES;      // 98304
+constexpr int P1 = 2 * HALO_BYTES + W_BYTES;  // 159744: both chunks resident, loaded up front
 constexpr int LDS = P1 > T_BYTES ? P1 : T_BYTES;
+constexpr int HALO_PER_WAVE = HALO_INSTR / WM;  // 15 glds per wave per chunk
+static_assert(HALO_INSTR % WM == 0 && W_INSTR % WM == 0, "even glds split keeps vmcnt counting exact");
 static_assert(TR * HC % 32 == 0, "");
 }  // namespace tail
 
@@ -176,8 +178,7 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
     const char* xbase = view_at(d.x, img, y0 - 4, x0 - 4, 0);
     const size_t pstride = plane_bytes(d.x);
     const int xrow = d.x.wp * 32;
-    char* halo = smem;
-    char* wl = smem + HALO_BYTES;
+    char* wl = smem + 2 * HALO_BYTES;
 
     f32x16 acc[RT];
 #pragma unroll
@@ -185,23 +186,31 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
 #pragma unroll
         for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
 
-#pragma unroll 1
-    for (int chunk = 0; chunk < 2; ++chunk) {
-        if (chunk == 0) {
-            for (int j = wave; j < W_INSTR; j += WM)
-                glds16((const char*)d.wpack + j * 1024 + lane * 16, wl + j * 1024);
-        }
-        // halo image [plane kp][pixel q][2 units], 32 pixels of one plane per glds
+    // Issue every load of the tile at once (weights, chunk-0 halo, chunk-1 halo) so the
+    // chunk-1 fetch overlaps the chunk-0 MFMAs.  Halo image per chunk: [plane kp][pixel q][2 units].
+    for (int j = wave; j < W_INSTR; j += WM)
+        glds16((const char*)d.wpack + j * 1024 + lane * 16, wl + j * 1024);
+#pragma unroll
+    for (int chunk = 0; chunk < 2; ++chunk)
         for (int j = wave; j < HALO_INSTR; j += WM) {
             const int kp = j / HIPL;
             const int u = (j - kp * HIPL) * 64 + lane;
             const int q = u >> 1;
             const int row = q / HC, col = q - row * HC;
             const int c = (u & 1) ^ ((q >> 3) & 1);
-            glds16(xbase + (size_t)(chunk * 2 + kp) * pstride + row * xrow + col * 32 + c * 16, halo + j * 1024);
+            glds16(xbase + (size_t)(chunk * 2 + kp) * pstride + row * xrow + col * 32 + c * 16,
+                   smem + chunk * HALO_BYTES + j * 1024);
         }
-        wait_vm0();
-        __syncthreads();
+
+#pragma unroll
+    for (int chunk = 0; chunk < 2; ++chunk) {
+        if (chunk == 0)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(HALO_PER_WAVE) : "memory");
+        else
+            wait_vm0();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const char* halo = smem + chunk * HALO_BYTES;
 #pragma unroll
         for (int kx = 0; kx < 9; ++kx) {
 #pragma unroll
@@ -216,8 +225,8 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
                 }
             }
         }
-        __syncthreads();
     }
+    __syncthreads();
 
     float* T = reinterpret_cast<float*>(smem);
 #pragma unroll

@@ -1,0 +1,211 @@
+"""Tiled uint8 super-resolution of large stills — the rs.py image branch
+(rs.py:16-27 `sliding_window`, rs.py:78-114 `runer` stitch), MI355X-first.
+
+Differences from the reference loop, none of which change its output in the
+halo=0 mode:
+
+* tiles of the same shape are batched (the reference runs batch 1), each shape
+  group through one pre-built `engine.GeneratorPlan` (uint8 in → uint8 out,
+  Normalize and TanhToArrayImage fused into the 9x9 head / tail kernels);
+* the image is uploaded once and tiles are cut on the GPU; the output canvas
+  lives in HBM and is copied to the host once;
+* tiles are pasted at (y·s, x·s).  For every image the reference's cursor
+  (rs.py:105-111: `width += w`, wrap at `image_width`) lands on exactly those
+  coordinates, because the windows of one row sum to the image width;
+* optional `halo` (cfg4: 32 px): each window is extended by `halo` LR pixels on
+  every side (clipped to the image, so the network still sees its own zero
+  padding at the true image border), run, and the core is cropped back out.
+  This removes the seams of the reference's halo-less stitching;
+* multi-GPU: tiles are dealt longest-processing-time-first
+  across ranks, no collective on the data path; rank 0 receives the finished
+  output tiles point-to-point.
+"""
+from __future__ import annotations
+
+import heapq
+from collections import defaultdict
+from dataclasses import dataclass
+from typing import Callable, Sequence
+
+import torch
+
+from . import engine
+
+
+@dataclass(frozen=True)
+class Tile:
+    """One rs.py window.  (y, x, h, w): the core window in LR pixels, as
+    `sliding_window` yields it; (y0, x0, y1, x1): the input region actually run
+    (core + halo, clipped to the image)."""
+    index: int
+    y: int
+    x: int
+    h: int
+    w: int
+    y0: int
+    x0: int
+    y1: int
+    x1: int
+
+    @property
+    def in_shape(self) -> tuple[int, int]:
+        return self.y1 - self.y0, self.x1 - self.x0
+
+    @property
+    def cost(self) -> int:
+        return (self.y1 - self.y0) * (self.x1 - self.x0)
+
+
+def plan_tiles(height: int, width: int, window: int, halo: int = 0) -> list[Tile]:
+    """Windows in the reference's raster order (rs.py:16-27): step = window
+    clamped to the image, the last row/column ragged."""
+    if window <= 0 or halo < 0:
+        raise ValueError("window must be > 0 and halo >= 0")
+    sy, sx = min(height, window), min(width, window)
+    tiles = []
+    for y in range(0, height, sy):
+        for x in range(0, width, sx):
+            h, w = min(window, height - y), min(window, width - x)
+            tiles.append(Tile(len(tiles), y, x, h, w, max(0, y - halo), max(0, x - halo),
+                              min(height, y + h + halo), min(width, x + w + halo)))
+    return tiles
+
+
+def shard_tiles(tiles: Sequence[Tile], world: int) -> list[list[Tile]]:
+    """Longest-processing-time-first deal of tiles over `world` ranks
+    (SURVEY.md §8e): biggest tile to the least-loaded rank.  Deterministic, so
+    every rank computes the same assignment without communicating."""
+    heap = [(0, r) for r in range(world)]
+    out: list[list[Tile]] = [[] for _ in range(world)]
+    for t in sorted(tiles, key=lambda t: (-t.cost, t.index)):
+        load, r = heapq.heappop(heap)
+        out[r].append(t)
+        heapq.heappush(heap, (load + t.cost, r))
+    for lst in out:
+        lst.sort(key=lambda t: t.index)
+    return out
+
+
+BatchRunner = Callable[[torch.Tensor], torch.Tensor]  # uint8 [b,3,h,w] → uint8 [b,3,s·h,s·w]
+
+
+class GeneratorRunner:
+    """uint8 batch runner on the HIP generator: one GeneratorPlan per (b, h, w)."""
+
+    def __init__(self, gw: engine.GeneratorWeights, mean, std, device):
+        self.gw, self.mean, self.std, self.device = gw, tuple(mean), tuple(std), torch.device(device)
+        self.scale = 2 ** len(gw.scalers)
+        self.plans: dict[tuple[int, int, int], engine.GeneratorPlan] = {}
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dtype != torch.uint8 or not x.is_cuda:
+            raise ValueError("GeneratorRunner expects a uint8 CUDA batch")
+        n, _, h, w = x.shape
+        plan = self.plans.get((n, h, w))
+        if plan is None:
+            plan = engine.GeneratorPlan(self.gw, n, h, w, self.device, True, True, self.mean, self.std)
+            self.plans[(n, h, w)] = plan
+        out = torch.empty(plan.out_shape, dtype=torch.uint8, device=self.device)
+        return plan.run(x.contiguous(), out)
+
+    def free(self):
+        self.plans.clear()
+
+
+def runner_for(model, device) -> GeneratorRunner:
+    """Build the HIP runner from the drop-in modules: a `Model` wrapper with
+    `init_normalize` (uint8 I/O), or a bare ResNet/EResNet/SRGAN generator with
+    ImageNet normalisation (utils/datasets.py:53 defaults)."""
+    from . import models
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    net = model
+    if isinstance(model, models.Model):
+        net = model.net
+        if isinstance(net, torch.nn.Sequential) and len(net) == 3 and isinstance(net[0], models.Normalize):
+            mean = tuple(net[0].mean.flatten().tolist())
+            std = tuple(net[0].std.flatten().tolist())
+            net = net[1]
+    if isinstance(net, models.SRGAN):
+        net = net.res_net
+    if not isinstance(net, models._Generator):
+        raise TypeError(f"tiled inference needs a ResNet/EResNet/SRGAN generator, got {type(net).__name__}")
+    return GeneratorRunner(net._packed(torch.device(device)), mean, std, device)
+
+
+class TileUpscaler:
+    """rs.py image branch as a reusable object.
+
+    `runner` maps uint8 [b,3,h,w] → uint8 [b,3,s·h,s·w] on `device` (the HIP
+    GeneratorRunner in production).  `batch` tiles of one shape run together.
+    """
+
+    def __init__(self, runner: BatchRunner, scale: int, window: int = 96, halo: int = 0, batch: int = 8,
+                 device="cuda"):
+        if batch < 1:
+            raise ValueError("batch must be >= 1")
+        self.runner, self.scale, self.window, self.halo, self.batch = runner, scale, window, halo, batch
+        self.device = torch.device(device)
+
+    def run_tiles(self, image: torch.Tensor, tiles: Sequence[Tile]) -> dict[int, torch.Tensor]:
+        """Upscale `tiles` of `image` (uint8 [3,H,W] on self.device); returns
+        {tile.index: uint8 [3, s·h, s·w] core output} (views into batch outputs)."""
+        s = self.scale
+        groups: dict[tuple[int, int], list[Tile]] = defaultdict(list)
+        for t in tiles:
+            groups[t.in_shape].append(t)
+        out: dict[int, torch.Tensor] = {}
+        for (h, w), lst in groups.items():
+            for i in range(0, len(lst), self.batch):
+                chunk = lst[i:i + self.batch]
+                x = torch.stack([image[:, t.y0:t.y1, t.x0:t.x1] for t in chunk])
+                y = self.runner(x)
+                if tuple(y.shape) != (len(chunk), 3, h * s, w * s):
+                    raise RuntimeError(f"runner returned {tuple(y.shape)} for a {len(chunk)}x3x{h}x{w} batch "
+                                       f"at scale {s}")
+                for j, t in enumerate(chunk):
+                    oy, ox = (t.y - t.y0) * s, (t.x - t.x0) * s
+                    out[t.index] = y[j, :, oy:oy + t.h * s, ox:ox + t.w * s]
+        return out
+
+    def __call__(self, image: torch.Tensor, rank: int = 0, world: int = 1, group=None) -> torch.Tensor | None:
+        """Upscale a uint8 [3,H,W] image.  With world > 1 (torch.distributed
+        initialised, every rank passing the same image), each rank runs its
+        share of the tiles and rank 0 returns the stitched [3,s·H,s·W] uint8
+        canvas (on self.device); other ranks return None."""
+        if image.dim() != 3 or image.dtype != torch.uint8:
+            raise ValueError("expected a uint8 CHW image")
+        c, H, W = image.shape
+        s = self.scale
+        image = image.to(self.device, non_blocking=True)
+        tiles = plan_tiles(H, W, self.window, self.halo)
+        mine = shard_tiles(tiles, world)[rank] if world > 1 else tiles
+        done = self.run_tiles(image, mine)
+        if world == 1:
+            canvas = torch.zeros((c, H * s, W * s), dtype=torch.uint8, device=self.device)
+            for t in tiles:
+                canvas[:, t.y * s:(t.y + t.h) * s, t.x * s:(t.x + t.w) * s] = done[t.index]
+            return canvas
+        return _gather_to_rank0(tiles, shard_tiles(tiles, world), done, s, (c, H * s, W * s), rank, group,
+                                self.device)
+
+
+def _gather_to_rank0(tiles, shards, done, s, canvas_shape, rank, group, device):
+    """Point-to-point collection of finished tiles on rank 0 (no data-path
+    collective).  gloo needs host tensors, RCCL device ones."""
+    import torch.distributed as dist
+    comm_dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else device
+    if rank != 0:
+        for t in shards[rank]:
+            dist.send(done[t.index].contiguous().to(comm_dev), dst=0, group=group)
+        return None
+    canvas = torch.zeros(canvas_shape, dtype=torch.uint8, device=device)
+    owner = {t.index: r for r, lst in enumerate(shards) for t in lst}
+    for r, lst in enumerate(shards):
+        for t in lst:
+            if r == 0:
+                part = done[t.index]
+            else:
+                part = torch.empty((canvas_shape[0], t.h * s, t.w * s), dtype=torch.uint8, device=comm_dev)
+                dist.recv(part, src=owner[t.index], group=group)
+            canvas[:, t.y * s:(t.y + t.h) * s, t.x * s:(t.x + t.w) * s] = part.to(device)
+    return canvas

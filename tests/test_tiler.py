@@ -1,0 +1,118 @@
+"""Host logic of the rs.py tiler (image_super_resolution_amd/tiler.py) on CPU:
+window planning, stitching, halo semantics and the multi-rank tile deal.
+
+The batch runner is injected (a deterministic uint8 operator), so these tests
+pin the tiler against the oracle's restatement of the reference stitch
+(oracle/ref_cpu.py:tiled_u8, rs.py:78-111) without needing a GPU; the HIP
+generator runner is covered in test_gpu_parity.py."""
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from image_super_resolution_amd import tiler
+from oracle import ref_cpu
+
+S = 4
+
+
+def box_up(x: torch.Tensor) -> torch.Tensor:
+    """uint8 [b,3,h,w] → uint8 [b,3,4h,4w]: 3x3 zero-padded box sum (radius 1,
+    so image-border semantics matter) then nearest x4 upsample."""
+    xf = x.float()
+    k = torch.ones(3, 1, 3, 3)
+    y = torch.nn.functional.conv2d(xf, k, padding=1, groups=3) / 9.0
+    y = y.round().clamp(0, 255).to(torch.uint8)
+    return y.repeat_interleave(S, -2).repeat_interleave(S, -1)
+
+
+def image(h, w, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, 256, (3, h, w), generator=g, dtype=torch.uint8)
+
+
+@pytest.mark.parametrize("h,w,window", [(37, 53, 16), (16, 16, 16), (10, 70, 32), (64, 40, 96), (1, 1, 4)])
+def test_plan_matches_sliding_window(h, w, window):
+    img = image(h, w)
+    ref = [(x, y, tuple(win.shape[-2:])) for _, x, y, win in ref_cpu.sliding_window(img, window)]
+    got = [(t.x, t.y, (t.h, t.w)) for t in tiler.plan_tiles(h, w, window)]
+    assert got == ref
+
+
+@pytest.mark.parametrize("h,w,window,batch", [(37, 53, 16, 1), (37, 53, 16, 5), (64, 40, 96, 8), (33, 33, 8, 3)])
+def test_halo0_matches_reference_stitch(h, w, window, batch):
+    img = image(h, w, seed=h * w)
+    ref = ref_cpu.tiled_u8(box_up, img, window)
+    up = tiler.TileUpscaler(box_up, S, window=window, halo=0, batch=batch, device="cpu")
+    assert torch.equal(up(img), ref)
+
+
+@pytest.mark.parametrize("halo", [1, 3])
+def test_halo_removes_seams(halo):
+    """With halo >= the operator's receptive radius, tiled == whole-image run."""
+    img = image(45, 61, seed=7)
+    full = box_up(img[None])[0]
+    up = tiler.TileUpscaler(box_up, S, window=16, halo=halo, batch=4, device="cpu")
+    assert torch.equal(up(img), full)
+    seams = tiler.TileUpscaler(box_up, S, window=16, halo=0, batch=4, device="cpu")(img)
+    assert not torch.equal(seams, full)
+
+
+def test_shard_lpt_balanced_and_complete():
+    tiles = tiler.plan_tiles(2160, 3840, 512, 32)  # cfg4: 40 tiles
+    assert len(tiles) == 40
+    for world in (1, 2, 3, 8):
+        shards = tiler.shard_tiles(tiles, world)
+        assert sorted(t.index for s in shards for t in s) == list(range(40))
+        loads = [sum(t.cost for t in s) for s in shards]
+        assert max(loads) - min(loads) <= max(t.cost for t in tiles)
+
+
+def test_runner_shape_check():
+    up = tiler.TileUpscaler(lambda x: x, S, window=8, device="cpu")
+    with pytest.raises(RuntimeError, match="runner returned"):
+        up(image(8, 8))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        img = image(45, 61, seed=11)
+        up = tiler.TileUpscaler(box_up, S, window=16, halo=2, batch=2, device="cpu")
+        out = up(img, rank=rank, world=world)
+        if rank == 0:
+            q.put(out)
+        else:
+            q.put(out is None)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_gloo_world2_matches_single():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    canvas = next(r for r in res if isinstance(r, torch.Tensor))
+    assert any(r is True for r in res)
+    img = image(45, 61, seed=11)
+    single = tiler.TileUpscaler(box_up, S, window=16, halo=2, batch=2, device="cpu")(img)
+    assert torch.equal(canvas, single)
