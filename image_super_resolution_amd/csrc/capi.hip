@@ -73,8 +73,8 @@ size_t isr_tail9x9_packed_bytes(int32_t cout, int32_t cin) { (void)cout; (void)c
 int isr_pack_conv3x3(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
     if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_conv3x3: null pointer");
     if (cin <= 0 || cin % 32) return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cin %d must be a positive multiple of 32", cin);
-    if (!(cout == 32 || (cout > 0 && cout % 64 == 0)))
-        return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cout %d must be 32 or a multiple of 64", cout);
+    if (cout <= 0 || cout % 32)
+        return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cout %d must be a positive multiple of 32", cout);
     return launched(isr::conv3x3_pack(w, packed, cout, cin, (hipStream_t)s), "pack_conv3x3");
 }
 
@@ -97,11 +97,24 @@ static int conv3x3_validate(const isr_conv_desc* d) {
         return fail(ISR_ERR_BAD_DESC, "conv3x3: computed region %dx%d must cover %dx%d and be a multiple of %dx%d", d->ha, d->wa,
                     d->h, d->w, ISR_TILE_H, ISR_TILE_W);
     if (d->cin <= 0 || d->cin % 32) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cin %d must be a multiple of 32", d->cin);
-    if (!(d->cout == 32 || (d->cout > 0 && d->cout % 64 == 0)))
-        return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cout %d must be 32 or a multiple of 64", d->cout);
+    if (d->cout <= 0 || d->cout % 32)
+        return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cout %d must be a positive multiple of 32", d->cout);
     if (!d->wpack) return fail(ISR_ERR_BAD_DESC, "conv3x3: null weights");
     if (d->shuffle != 1 && d->shuffle != 2) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: shuffle must be 1 or 2");
-    if (!view_ok(d->x, d->ha, d->wa, 1, d->cin, "conv3x3.x", 1)) return ISR_ERR_BAD_DESC;
+    if (d->x_sub2) {
+        if (d->cin % 128) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: x_sub2 needs cin %% 128 == 0 (got %d)", d->cin);
+        if (d->shuffle != 1) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: x_sub2 with a shuffled store");
+        if (!view_ok(d->x, 2 * d->ha, 2 * d->wa, 2, d->cin / 4, "conv3x3.x", 1)) return ISR_ERR_BAD_DESC;
+    } else if (!view_ok(d->x, d->ha, d->wa, 1, d->cin, "conv3x3.x", 1)) {
+        return ISR_ERR_BAD_DESC;
+    }
+    if (d->m.data) {
+        if (d->shuffle != 1 || d->y2.data)
+            return fail(ISR_ERR_UNSUPPORTED, "conv3x3: mask epilogue takes no shuffle / second output");
+        if (d->m_c0 < 0 || d->m_c0 % 32) return fail(ISR_ERR_BAD_DESC, "conv3x3: m_c0 %d must be a multiple of 32", d->m_c0);
+        if (!view_ok(d->m, d->ha, d->wa, 0, d->cout, "conv3x3.m", 1)) return ISR_ERR_BAD_DESC;
+    }
+    if (d->r1_cn < 0 || d->r1_cn % 32) return fail(ISR_ERR_BAD_DESC, "conv3x3: r1_cn %d must be a multiple of 32", d->r1_cn);
     if (d->shuffle == 2) {
         if (d->cout % 64) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: pixel shuffle needs cout %% 64 == 0");
         if (d->r1.data || d->r2.data || d->y2.data)

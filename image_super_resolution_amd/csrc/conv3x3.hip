@@ -72,7 +72,9 @@ __device__ __forceinline__ void swap_halves(float& lo, float& hi) {
 //    output may alias a residual: the in-place RRDB update).
 //  * PixelShuffle(2) (MODE 8): transpose through LDS one row at a time, so a
 //    lane stores 8 channels of one shuffled output pixel.
-// MODE bits (compile-time: no per-element branches): 1 = r1, 2 = r2, 4 = y2, 8 = shuffle.
+// MODE bits (compile-time: no per-element branches): 1 = r1, 2 = r2, 4 = y2, 8 = shuffle,
+// 16 = LeakyReLU' mask (backward).  r1_cn / m_c0 are multiples of 32, so their
+// channel tests are uniform per 32-cout fragment (scalar branches).
 template <class C, int MODE>
 __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C::R][C::NF], int img, int ct,
                                          int x0, int y0, int wave, int lane) {
@@ -125,12 +127,20 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
             const bool valid = yy < d.h && xx < d.w;
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
-                bf16x8 q1[2], q2[2]; // residuals of this fragment, loaded before its stores
+                bf16x8 q1[2], q2[2], qm[2]; // residuals / mask of this fragment, loaded before its stores
+                const int cf = ct * CT + f * 32;
+                const bool use_r1 = (MODE & 1) && (d.r1_cn == 0 || cf < d.r1_cn);
+                const bool use_m = (MODE & 16) && cf >= d.m_c0;
 #pragma unroll
                 for (int blk = 0; blk < 2; ++blk) {
-                    const int co = ct * CT + f * 32 + 16 * blk + 8 * hh;
-                    if constexpr (MODE & 1) q1[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r1, img, yy, xx, co));
+                    const int co = cf + 16 * blk + 8 * hh;
+                    if constexpr (MODE & 1) {
+                        if (use_r1) q1[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r1, img, yy, xx, co));
+                    }
                     if constexpr (MODE & 2) q2[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r2, img, yy, xx, co));
+                    if constexpr (MODE & 16) {
+                        if (use_m) qm[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.m, img, yy, xx, co));
+                    }
                 }
                 float v[16];
 #pragma unroll
@@ -147,8 +157,11 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
-                        if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (float)q1[blk][e];
+                        if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (use_r1 ? (float)q1[blk][e] : 0.f);
                         if constexpr (MODE & 2) u[e] = u[e] * d.s2 + (float)q2[blk][e];
+                        if constexpr (MODE & 16) {
+                            if (use_m && !((float)qm[blk][e] > 0.f)) u[e] *= d.mslope;
+                        }
                         if (!valid) u[e] = 0.f;
                     }
                     const int co = ct * CT + f * 32 + 16 * blk + 8 * hh;
@@ -183,10 +196,21 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     const int nchunks = C::CIN ? C::CIN / C::KC : d.cin / C::KC;
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
-    const char* xbase = view_at(d.x, img, y0 - 1, x0 - 1, 0);
+    // x_sub2 (backward of PixelShuffle): halo pixel (row, col) of sub-position s
+    // lives at x pixel (2row + (s>>1), 2col + (s&1)) — pixel stride 2 plus a
+    // per-chunk offset.
+    const int ps = d.x_sub2 ? 2 : 1;
+    const char* xbase = view_at(d.x, img, ps * (y0 - 1), ps * (x0 - 1), 0);
     const size_t pstride = plane_bytes(d.x);
     const char* wbase = (const char*)d.wpack;
     const int xrow_bytes = d.x.wp * 32;
+    auto xchunk = [&](int chunk) -> size_t {
+        if (!d.x_sub2) return (size_t)chunk * C::KS * pstride;
+        const int cs4 = d.cin >> 2;
+        const int c0 = chunk * C::KC;
+        const int sp = c0 / cs4, cb = (c0 - sp * cs4) >> 4;
+        return (size_t)cb * pstride + (size_t)(sp >> 1) * xrow_bytes + (sp & 1) * 32;
+    };
     const size_t wchunk_bytes = (size_t)C::KS * 9 * d.cout * 32;
     uint32_t off[C::IPW];
 #pragma unroll
@@ -201,7 +225,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
                 const int row = q / C::HC;
                 const int col = q - row * C::HC;
                 const int c = (u & 1) ^ ((q >> 3) & 1);
-                o = (uint32_t)(kp * pstride + row * xrow_bytes + col * 32 + c * 16);
+                o = (uint32_t)(kp * pstride + ps * (row * xrow_bytes + col * 32) + c * 16);
             }
         } else if (j < C::INSTR) {
             const int u = (j - C::HALO_INSTR) * 64 + lane;
@@ -214,7 +238,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
 
     auto stage = [&](int chunk, int buf) {
         char* dst = smem + buf * C::STAGE;
-        const char* xs = xbase + (size_t)chunk * C::KS * pstride;
+        const char* xs = xbase + xchunk(chunk);
         const char* ws = wbase + (size_t)chunk * wchunk_bytes;
 #pragma unroll
         for (int k = 0; k < C::IPW; ++k) {
@@ -329,7 +353,8 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         return;
     }
     // ---- epilogue (mode picked once, wave-uniform, so no per-element branches)
-    const int mode = d.shuffle == 2 ? 8 : ((d.r1.data ? 1 : 0) | (d.r2.data ? 2 : 0) | (d.y2.data ? 4 : 0));
+    const int mode = d.shuffle == 2 ? 8
+                                    : ((d.r1.data ? 1 : 0) | (d.r2.data ? 2 : 0) | (d.y2.data ? 4 : 0) | (d.m.data ? 16 : 0));
     switch (mode) {
         case 0: epilogue<C, 0>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 1: epilogue<C, 1>(d, acc, img, ct, x0, y0, wave, lane); break;
@@ -339,7 +364,11 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         case 5: epilogue<C, 5>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 6: epilogue<C, 6>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 7: epilogue<C, 7>(d, acc, img, ct, x0, y0, wave, lane); break;
-        default: epilogue<C, 8>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 8: epilogue<C, 8>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 16: epilogue<C, 16>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 17: epilogue<C, 17>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 18: epilogue<C, 18>(d, acc, img, ct, x0, y0, wave, lane); break;
+        default: epilogue<C, 19>(d, acc, img, ct, x0, y0, wave, lane); break;  // 19; y2 + mask is rejected by isr_conv3x3_fwd
     }
 }
 
@@ -375,7 +404,7 @@ using V_W3 = C3<4, 4, 2, 32, 2>; // 16x32, KC32, 1 block / CU
 using V_F0 = C3<4, 4, 2, 16, 2, 192>; // RDB final conv 192→64: V_W0 with compile-time cin
 
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
-    if (d->cout == 32) {
+    if (d->cout % 64) {  // 32-cout tiles: growth convs (cout 32) and dgrad of them (96, 160)
         switch (variant) {
             case 0: return launch3x3<V_G0>(d, s);
             case 1: return launch3x3<V_G1>(d, s);

@@ -137,8 +137,14 @@ def conv3x3_desc(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor
                  y: ActBuffer, *, x_coff: int = 0, y_coff: int = 0, slope: float = 1.0,
                  r1: ActBuffer | None = None, r1_coff: int = 0, s1: float = 1.0,
                  r2: ActBuffer | None = None, r2_coff: int = 0, s2: float = 1.0,
-                 y2: ActBuffer | None = None, y2_coff: int = 0, shuffle: int = 1) -> IsrConvDesc:
-    """Descriptor for y[..., y_coff:y_coff+cout] = epilogue(conv3x3(x[..., x_coff:x_coff+cin]))."""
+                 y2: ActBuffer | None = None, y2_coff: int = 0, shuffle: int = 1,
+                 m: ActBuffer | None = None, m_coff: int | None = None, mslope: float = 1.0, m_c0: int = 0,
+                 r1_cn: int = 0, x_sub2: bool = False) -> IsrConvDesc:
+    """Descriptor for y[..., y_coff:y_coff+cout] = epilogue(conv3x3(x[..., x_coff:x_coff+cin])).
+
+    Backward extensions: `m` (read at channel m_coff, default y_coff) masks output
+    channels >= m_c0 with LeakyReLU'(m) of slope `mslope`; `r1_cn` limits r1 to the
+    first r1_cn output channels; `x_sub2` reads x (2h x 2w grid) as PixelShuffle(2)ᵀ."""
     d = IsrConvDesc()
     d.n, d.h, d.w, d.ha, d.wa = x.n, x.h, x.w, x.ha, x.wa
     d.cin, d.cout = cin, cout
@@ -150,6 +156,10 @@ def conv3x3_desc(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor
     d.wpack = wpack.data_ptr()
     d.bias = bias.data_ptr() if bias is not None else None
     d.slope, d.s1, d.s2, d.shuffle = slope, s1, s2, shuffle
+    if x_sub2:
+        d.n, d.h, d.w, d.ha, d.wa = y.n, y.h, y.w, y.ha, y.wa
+    d.m = m.view(y_coff if m_coff is None else m_coff) if m is not None else _NULL_VIEW
+    d.mslope, d.m_c0, d.r1_cn, d.x_sub2 = mslope, m_c0, r1_cn, int(bool(x_sub2))
     return d
 
 

@@ -64,7 +64,7 @@ typedef struct isr_view {
 typedef struct isr_conv_desc {
     int32_t n, h, w;   /* batch; valid conv height/width (input == output size) */
     int32_t ha, wa;    /* computed (tile-aligned) extent; ha % 32 == 0, wa % 32 == 0 */
-    int32_t cin, cout; /* cin % 32 == 0; cout == 32 or cout % 64 == 0 */
+    int32_t cin, cout; /* cin % 32 == 0; cout % 32 == 0 (cout % 64 != 0 runs 32-cout tiles) */
     isr_view x;        /* input (cin channels from x.coff) */
     isr_view y;        /* output; for shuffle == 2 its grid is (2h, 2w), cout/4 channels */
     isr_view y2;       /* optional duplicate output (y2.data == NULL → none) */
@@ -73,6 +73,18 @@ typedef struct isr_conv_desc {
     const float* bias; /* [cout] fp32 or NULL */
     float slope, s1, s2;
     int32_t shuffle;   /* 1 = plain store, 2 = PixelShuffle(2) store */
+    /* Backward-pass extensions (all zero in the forward).  The epilogue order is
+     * v = act(acc + bias); v = v*s1 + r1; v = v*s2 + r2; v *= mask; store.
+     * Used by the generator backward (utils/models.py forward graph, autograd
+     * of train.py:57 / :102): input-gradient convs accumulate into the dense-block
+     * gradient buffer and apply LeakyReLU' of the forward activation. */
+    isr_view m;        /* optional mask source (data == NULL → none), same grid as y */
+    float mslope;      /* output channel c >= m_c0 is multiplied by (m[c] > 0 ? 1 : mslope) */
+    int32_t m_c0;      /* first masked output channel, multiple of 32 */
+    int32_t r1_cn;     /* r1 is added only to output channels < r1_cn (0 → all); multiple of 32 */
+    int32_t x_sub2;    /* 1: input channel c' = s*(cin/4) + c reads x at pixel (2y + (s>>1), 2x + (s&1)),
+                          channel c (x is on the 2h x 2w grid, pad >= 2): the transpose of
+                          PixelShuffle(2) (utils/models.py:583) folded into the load; cin % 128 == 0 */
 } isr_conv_desc;
 
 /* 9x9 head conv, 3 → cout (=64) channels, input NCHW (fp32 already normalised,

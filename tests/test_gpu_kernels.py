@@ -170,3 +170,59 @@ def test_bad_descriptor_raises():
     y = ops.ActBuffer.alloc(1, 16, 32, 64, 1, DEV)
     with pytest.raises(_lib.IsrError, match="multiple of 32"):
         ops.conv3x3(x, 48, torch.zeros(10, dtype=torch.bfloat16, device=DEV), None, 64, y)
+
+
+def test_conv3x3_backward_epilogue_mask_and_limited_residual():
+    """dgrad-style launch: r1 added to the first r1_cn channels only, LeakyReLU'
+    mask (from a forward activation buffer) on channels >= m_c0."""
+    from image_super_resolution_amd import ops
+    n, h, w, cin, cout = 2, 20, 36, 64, 192
+    x = _mk(n, cin, h, w, 21)
+    W = _w(cout, cin, 3, 22)
+    r = _mk(n, cout, h, w, 23)
+    act = _mk(n, cout, h, w, 24)
+    xb = ops.ActBuffer.from_nchw(x, pad=1)
+    rb = ops.ActBuffer.from_nchw(r, pad=1)
+    mb = ops.ActBuffer.from_nchw(act, pad=1)
+    yb = ops.ActBuffer.alloc(n, h, w, cout, 1, DEV)
+    ops.conv3x3(xb, cin, ops.pack_conv3x3(W), None, cout, yb, r1=rb, r1_cn=64, m=mb, m_c0=160, mslope=0.01)
+    torch.cuda.synchronize()
+    ref = F.conv2d(bf(x), bf(W), padding=1)
+    ref[:, :64] += bf(r)[:, :64]
+    ref[:, 160:] *= torch.where(bf(act)[:, 160:] > 0, 1.0, 0.01)
+    close(yb.to_nchw(), ref)
+    assert yb.outside_valid().float().abs().max().item() == 0.0
+
+
+def test_conv3x3_in_place_accumulate_with_mask():
+    """RDB dgrad step: G[0:cout] += conv(G[cin slot]) in place, last 32 channels masked."""
+    from image_super_resolution_amd import ops
+    n, h, w = 1, 18, 40
+    g = _mk(n, 192, h, w, 31)
+    act = _mk(n, 192, h, w, 32)
+    gb = ops.ActBuffer.from_nchw(g, pad=1)
+    mb = ops.ActBuffer.from_nchw(act, pad=1)
+    W = _w(160, 32, 3, 33)
+    ops.conv3x3(gb, 32, ops.pack_conv3x3(W), None, 160, gb, x_coff=160, r1=gb, m=mb, m_c0=128, mslope=0.2)
+    torch.cuda.synchronize()
+    ref = F.conv2d(bf(g)[:, 160:], bf(W), padding=1) + bf(g)[:, :160]
+    ref[:, 128:] *= torch.where(bf(act)[:, 128:160] > 0, 1.0, 0.2)
+    close(gb.to_nchw(0, 160), ref)
+    assert torch.equal(gb.to_nchw(160, 192), bf(g)[:, 160:])
+
+
+@pytest.mark.parametrize("h,w", [(16, 32), (20, 36), (40, 24)])
+def test_conv3x3_x_sub2_is_pixel_unshuffle(h, w):
+    """Input read as PixelShuffle(2)ᵀ of a 2h x 2w buffer (scaler backward)."""
+    from image_super_resolution_amd import ops
+    n, cs, cout = 2, 64, 64
+    g = _mk(n, cs, 2 * h, 2 * w, 41)
+    Wu = _w(cout, 4 * cs, 3, 42)  # weights over pixel_unshuffle channel order 4c + 2i + j
+    lr = ops.ActBuffer.alloc(n, h, w, cout, 1, DEV)
+    gb = ops.ActBuffer.alloc(n, 2 * h, 2 * w, cs, 2, DEV, ha=2 * lr.ha, wa=2 * lr.wa)
+    gb.set_nchw(g, 0)
+    Wk = Wu.view(cout, cs, 4, 3, 3).transpose(1, 2).reshape(cout, 4 * cs, 3, 3).contiguous()
+    ops.conv3x3(gb, 4 * cs, ops.pack_conv3x3(Wk), None, cout, lr, x_sub2=True)
+    torch.cuda.synchronize()
+    ref = F.conv2d(F.pixel_unshuffle(bf(g), 2), bf(Wu), padding=1)
+    close(lr.to_nchw(), ref)
