@@ -35,7 +35,8 @@ class IsrHeadDesc(ctypes.Structure):
     _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
                 ("cout", c_int32), ("x", c_void_p), ("x_u8", c_int32),
                 ("mean", c_float * 3), ("inv_std", c_float * 3),
-                ("y", IsrView), ("y2", IsrView), ("wpack", c_void_p), ("bias", c_void_p), ("slope", c_float)]
+                ("y", IsrView), ("y2", IsrView), ("wpack", c_void_p), ("bias", c_void_p), ("slope", c_float),
+                ("m", IsrView), ("mslope", c_float)]
 
 
 class IsrTailDesc(ctypes.Structure):
@@ -44,10 +45,27 @@ class IsrTailDesc(ctypes.Structure):
                 ("y", c_void_p), ("y_u8", c_int32)]
 
 
+class IsrWgradDesc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
+                ("cin", c_int32), ("cout", c_int32), ("x", IsrView), ("g", IsrView), ("g_sub2", c_int32),
+                ("scale", c_float), ("dw", c_void_p), ("db", c_void_p), ("splits", c_int32)]
+
+
+class IsrWgrad9Desc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
+                ("head", c_int32), ("p", c_void_p), ("q", IsrView), ("scale", c_float),
+                ("dw", c_void_p), ("db", c_void_p), ("splits", c_int32)]
+
+
 # Every symbol include/isr.h declares, with its ctypes signature.
 SIGNATURES = {
     "isr_conv3x3_packed_bytes": (c_size_t, [c_int32, c_int32]),
     "isr_pack_conv3x3": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "isr_pack_conv3x3_dgrad": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_float, c_int32, c_void_p]),
+    "isr_wgrad3x3_workspace_bytes": (c_size_t, [POINTER(IsrWgradDesc)]),
+    "isr_wgrad3x3": (c_int32, [POINTER(IsrWgradDesc), c_void_p, c_size_t, c_void_p]),
+    "isr_wgrad9x9_workspace_bytes": (c_size_t, [POINTER(IsrWgrad9Desc)]),
+    "isr_wgrad9x9": (c_int32, [POINTER(IsrWgrad9Desc), c_void_p, c_size_t, c_void_p]),
     "isr_head9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),
     "isr_pack_head9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "isr_tail9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),

@@ -18,6 +18,11 @@ size_t head9x9_packed_bytes(int cout);
 size_t tail9x9_packed_bytes();
 int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
+int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale, int sub2, hipStream_t s);
+size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
+size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
+int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
+int wgrad3x3_dispatch(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
 }  // namespace isr
 
 static thread_local char g_err[512] = "";
@@ -76,6 +81,15 @@ int isr_pack_conv3x3(const float* w, void* packed, int32_t cout, int32_t cin, is
     if (cout <= 0 || cout % 32)
         return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cout %d must be a positive multiple of 32", cout);
     return launched(isr::conv3x3_pack(w, packed, cout, cin, (hipStream_t)s), "pack_conv3x3");
+}
+
+int isr_pack_conv3x3_dgrad(const float* w, void* packed, int32_t cout, int32_t cin, float scale, int32_t sub2,
+                           isr_stream_t s) {
+    if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_conv3x3_dgrad: null pointer");
+    if (cin <= 0 || cin % 32 || cout <= 0 || cout % 32)
+        return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3_dgrad: cin %d / cout %d must be multiples of 32", cin, cout);
+    if (sub2 && cout % 128) return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3_dgrad: sub2 needs cout %% 128 == 0");
+    return launched(isr::conv3x3_pack_dgrad(w, packed, cout, cin, scale, sub2, (hipStream_t)s), "pack_conv3x3_dgrad");
 }
 
 int isr_pack_head9x9(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
@@ -153,6 +167,7 @@ int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s) {
     if (!d->x || !d->wpack) return fail(ISR_ERR_BAD_DESC, "head9x9: null input or weights");
     if (!view_ok(d->y, d->ha, d->wa, 0, 64, "head9x9.y", 1)) return ISR_ERR_BAD_DESC;
     if (d->y2.data && !view_ok(d->y2, d->ha, d->wa, 0, 64, "head9x9.y2", 1)) return ISR_ERR_BAD_DESC;
+    if (d->m.data && !view_ok(d->m, d->ha, d->wa, 0, 64, "head9x9.m", 1)) return ISR_ERR_BAD_DESC;
     if (d->bias && ((uintptr_t)d->bias % 16)) return fail(ISR_ERR_BAD_DESC, "head9x9: bias must be 16-byte aligned");
     return launched(isr::head9x9_fwd_dispatch(d, (hipStream_t)s), "head9x9");
 }
@@ -166,6 +181,65 @@ int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s) {
     if (!d->y || !d->wpack) return fail(ISR_ERR_BAD_DESC, "tail9x9: null output or weights");
     if (!view_ok(d->x, d->ha, d->wa, 4, 64, "tail9x9.x", 1)) return ISR_ERR_BAD_DESC;
     return launched(isr::tail9x9_fwd_dispatch(d, (hipStream_t)s), "tail9x9");
+}
+
+static int wgrad_validate(const isr_wgrad_desc* d) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: empty problem");
+    if (d->ha % ISR_TILE_H || d->wa % ISR_TILE_W || d->ha < d->h || d->wa < d->w)
+        return fail(ISR_ERR_BAD_DESC, "wgrad3x3: bad computed region %dx%d for %dx%d", d->ha, d->wa, d->h, d->w);
+    if (d->cin <= 0 || d->cin % 32 || d->cout <= 0 || d->cout % 32)
+        return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: cin %d / cout %d must be multiples of 32", d->cin, d->cout);
+    if (!d->dw) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null dw");
+    if (d->splits < 0) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: negative split count");
+    if (!view_ok(d->x, d->ha, d->wa, 1, d->cin, "wgrad3x3.x", 1)) return ISR_ERR_BAD_DESC;
+    if (d->g_sub2) {
+        if (d->cout % 128) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: g_sub2 needs cout %% 128 == 0");
+        if (!view_ok(d->g, 2 * d->ha, 2 * d->wa, 0, d->cout / 4, "wgrad3x3.g", 1)) return ISR_ERR_BAD_DESC;
+    } else if (!view_ok(d->g, d->ha, d->wa, 0, d->cout, "wgrad3x3.g", 1)) {
+        return ISR_ERR_BAD_DESC;
+    }
+    return ISR_OK;
+}
+
+size_t isr_wgrad3x3_workspace_bytes(const isr_wgrad_desc* d) {
+    if (wgrad_validate(d) != ISR_OK) return 0;
+    return isr::wgrad3x3_workspace_bytes(d);
+}
+
+int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
+    int rc = wgrad_validate(d);
+    if (rc != ISR_OK) return rc;
+    if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null workspace");
+    rc = isr::wgrad3x3_dispatch(d, workspace, ws_bytes, (hipStream_t)s);
+    if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: workspace of %zu bytes is smaller than %zu", ws_bytes,
+                              isr::wgrad3x3_workspace_bytes(d));
+    return launched(rc, "wgrad3x3");
+}
+
+static int wgrad9_validate(const isr_wgrad9_desc* d) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "wgrad9x9: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0) return fail(ISR_ERR_BAD_DESC, "wgrad9x9: empty problem");
+    if (d->ha % ISR_TILE_H || d->wa % ISR_TILE_W || d->ha < d->h || d->wa < d->w)
+        return fail(ISR_ERR_BAD_DESC, "wgrad9x9: bad computed region %dx%d for %dx%d", d->ha, d->wa, d->h, d->w);
+    if (!d->p || !d->dw) return fail(ISR_ERR_BAD_DESC, "wgrad9x9: null p / dw");
+    if (d->splits < 0) return fail(ISR_ERR_BAD_DESC, "wgrad9x9: negative split count");
+    if (!view_ok(d->q, d->ha, d->wa, d->head ? 0 : 4, 64, "wgrad9x9.q", 1)) return ISR_ERR_BAD_DESC;
+    return ISR_OK;
+}
+
+size_t isr_wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d) {
+    if (wgrad9_validate(d) != ISR_OK) return 0;
+    return isr::wgrad9x9_workspace_bytes(d);
+}
+
+int isr_wgrad9x9(const isr_wgrad9_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
+    int rc = wgrad9_validate(d);
+    if (rc != ISR_OK) return rc;
+    if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad9x9: null workspace");
+    rc = isr::wgrad9x9_dispatch(d, workspace, ws_bytes, (hipStream_t)s);
+    if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad9x9: workspace too small");
+    return launched(rc, "wgrad9x9");
 }
 
 }  // extern "C"

@@ -435,28 +435,54 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
 int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) { return conv3x3_fwd_variant(d, 0, s); }
 
 // ---- weight packing: fp32 OIHW → bf16 [c16][tap][cout][hpos][8] -----------
-__global__ void pack3x3_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
-    const size_t total = (size_t)cout * cin * 9;
+// Forward: the packed conv has (cout, cin) = the layer's, element W[n][ci][tap].
+// dgrad (transposed): the packed conv maps the layer's output gradient (cin' =
+// layer cout) to its input gradient (cout' = layer cin): element
+// scale * W[co(ci')][n][8 - tap] (180° rotation), where with sub2 the input
+// channel ci' = s*(layer cout/4) + c stands for layer channel co = 4c + s
+// (PixelShuffle order, see isr_conv_desc.x_sub2).
+__global__ void pack3x3_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int pcout, int pcin,
+                               int transposed, int sub2, float scale) {
+    const size_t total = (size_t)pcout * pcin * 9;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
         size_t rem = idx;
         const int e = rem % 8; rem /= 8;
         const int hpos = rem % 2; rem /= 2;
-        const int n = rem % cout; rem /= cout;
+        const int n = rem % pcout; rem /= pcout;
         const int tap = rem % 9; rem /= 9;
         const int c16 = (int)rem;
         const int h = hpos ^ ((n >> 3) & 1);
         const int ci = c16 * 16 + h * 8 + e;
-        out[idx] = (__bf16)w[((size_t)n * cin + ci) * 9 + tap];
+        float v;
+        if (!transposed) {
+            v = w[((size_t)n * pcin + ci) * 9 + tap];
+        } else {
+            const int cs4 = pcin >> 2;
+            const int co = sub2 ? (ci % cs4) * 4 + ci / cs4 : ci;  // layer output channel
+            v = w[((size_t)co * pcout + n) * 9 + (8 - tap)];       // layer W[co][n][8 - tap]; layer cin = pcout
+        }
+        out[idx] = (__bf16)(v * scale);
     }
 }
 
 size_t conv3x3_packed_bytes(int cout, int cin) { return (size_t)cout * cin * 9 * 2; }
 
-int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s) {
-    const size_t total = conv3x3_packed_bytes(cout, cin) / 2;
+static int pack_launch(const float* w, void* out, int pcout, int pcin, int transposed, int sub2, float scale,
+                       hipStream_t s) {
+    const size_t total = conv3x3_packed_bytes(pcout, pcin) / 2;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    hipLaunchKernelGGL(pack3x3_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)out, cout, cin);
+    hipLaunchKernelGGL(pack3x3_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)out, pcout, pcin, transposed, sub2,
+                       scale);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s) {
+    return pack_launch(w, out, cout, cin, 0, 0, 1.f, s);
+}
+
+// layer weights [cout][cin][3][3] → packed dgrad conv (cout' = cin, cin' = cout)
+int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale, int sub2, hipStream_t s) {
+    return pack_launch(w, out, cin, cout, 1, sub2, scale, s);
 }
 
 }  // namespace isr

@@ -115,6 +115,7 @@ __global__ __launch_bounds__(256) void head9x9_kernel(isr_head_desc d) {
     Epi e;
     e.bias = d.bias; e.slope = d.slope; e.s1 = 1.f; e.s2 = 1.f;
     e.y = d.y; e.y2 = d.y2; e.r1.data = nullptr; e.r2.data = nullptr; e.h = d.h; e.w = d.w;
+    e.m = d.m; e.mslope = d.mslope;
     constexpr int CG = CT / 8;
 #pragma unroll 4
     for (int it = 0; it < R * CT / 16; ++it) {

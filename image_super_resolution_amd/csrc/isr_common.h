@@ -78,11 +78,13 @@ __device__ __forceinline__ void store8_bf16(char* p, const float* v) {
 }
 
 // Fused epilogue on 8 consecutive output channels [co, co+8) of one pixel.
-// v = leaky(v + bias); v = v*s1 + r1; v = v*s2 + r2; zero outside the valid region.
+// v = leaky(v + bias); v = v*s1 + r1; v = v*s2 + r2; v *= LeakyReLU'(m) (backward);
+// zero outside the valid region.
 struct Epi {
     const float* bias;
     float slope, s1, s2;
-    isr_view y, y2, r1, r2;
+    isr_view y, y2, r1, r2, m;
+    float mslope;
     int h, w;
 };
 
@@ -107,6 +109,12 @@ __device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int 
         load8_bf16(view_at(e.r2, img, yy, xx, co), r);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = v[k] * e.s2 + r[k];
+    }
+    if (e.m.data) {
+        float m[8];
+        load8_bf16(view_at(e.m, img, yy, xx, co), m);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = m[k] > 0.f ? v[k] : v[k] * e.mslope;
     }
     if (!valid) {
 #pragma unroll

@@ -1,0 +1,308 @@
+// Weight (and bias) gradient of a 3x3 'same' conv on CDNA4 MFMA — the
+// bwd-weight half of autograd through Conv / ConvWithoutBN / RDB / Scaler
+// (utils/models.py:75-111, 174-199, 245-271, 572-589; backward of train.py:57, :102).
+//
+//   dW[co][ci][dy][dx] = scale * sum_{n,y,x} G[n][co][y][x] * X[n][ci][y+dy-1][x+dx-1]
+//   db[co]             = scale * sum_{n,y,x} G[n][co][y][x]
+//
+// GEMM view: M = cout (from G), N = cin (from X, shifted per tap), K = pixels.
+// Both operands are channel-blocked [N][C/16][H][W][16] bf16, i.e. pixel-major
+// with 16 channels per 32-byte unit, while the MFMA wants 8 consecutive K
+// (pixels) per lane for one M/N index (channel): tiles are staged to LDS
+// unchanged (global_load_lds, lane-linear) and read with ds_read_b64_tr_b16,
+// the gfx950 transposing LDS read (cdna_hip_programming.md T10), which turns a
+// [pixel][channel] image into per-channel pixel runs for free.
+//
+// Block = 3 waves; wave w owns kernel row dy = w and all three dx taps, for a
+// CO_T x CI_T (co, ci) tile: 3 * NCO * NCI accumulators of 32x32.  The A
+// fragment (G, 32 co x 16 px) is reused by the 3 taps of the wave; the B
+// fragment (X shifted by (dy, dx)) is read per tap.  Pixel tiles are TY rows x
+// 32 columns; each block walks a contiguous range of them (split-K over
+// n*h*w), double-buffered through LDS.  Per-block partial sums go to a
+// workspace [split][tap][co][ci] (+ [split][co] for the bias); a second kernel
+// reduces over splits, applies `scale`, and writes dW in the reference OIHW
+// layout (and un-permutes the PixelShuffle channel order for g_sub2).
+#include "isr_common.h"
+
+namespace isr {
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+
+// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group passes the address of
+// pixel-row q, channels 4p..4p+3; lane i of the group receives channel i of
+// the 4 pixels.
+__device__ __forceinline__ bf16x4 lds_tr4(const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(p));
+}
+
+__device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
+    return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int NCO_, int NCI_, int TY_>
+struct WG {
+    static constexpr int NCO = NCO_, NCI = NCI_, TY = TY_;
+    static constexpr int WM = 3, NT = 64 * WM;
+    static constexpr int CO_T = 32 * NCO, CI_T = 32 * NCI;
+    static constexpr int GPL = 2 * NCO, XPL = 2 * NCI;         // 16-channel planes per stage
+    static constexpr int XPIX = (TY + 2) * 34;                  // halo pixels per plane
+    static constexpr int G_IPL = TY;                            // glds per G plane (one row each)
+    static constexpr int X_IPL = (XPIX * 2 + 63) / 64;          // glds per X plane
+    // plane strides = 128 (mod 256) bytes: the two 16-lane groups of a half-wave
+    // read the same pixels of planes 2e and 2e+1 → disjoint bank halves.
+    static constexpr int G_PLANE = G_IPL * 1024 + 128;
+    static constexpr int X_PLANE = X_IPL * 1024 + 128;
+    static constexpr int G_BYTES = GPL * G_PLANE;
+    static constexpr int STAGE = G_BYTES + XPL * X_PLANE;
+    static constexpr int G_INSTR = GPL * G_IPL, INSTR = G_INSTR + XPL * X_IPL;
+    static constexpr int IPW = (INSTR + WM - 1) / WM;
+    static constexpr int LDS = 2 * STAGE;
+    static_assert(LDS <= 163840, "LDS budget");
+};
+
+struct WgradArgs {
+    isr_wgrad_desc d;
+    float* ws;  // [splits][9][cout][cin] then [splits][cout]
+    int splits, tiles;
+};
+
+template <class C>
+__global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const isr_wgrad_desc& d = a.d;
+    constexpr int NCO = C::NCO, NCI = C::NCI, TY = C::TY;
+    const int ncot = d.cout / C::CO_T, ncit = d.cin / C::CI_T;
+    int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int cit = b % ncit; b /= ncit;
+    const int cot = b % ncot; b /= ncot;
+    const int split = b;
+    const int t0 = (int)((long)split * a.tiles / a.splits), t1 = (int)((long)(split + 1) * a.tiles / a.splits);
+    const int wave = wave_id();  // = dy
+    const int lane = threadIdx.x & 63;
+    const int nbx = d.wa / 32, nby = d.ha / TY;
+
+    // ---- per-lane glds offsets relative to the tile bases (tile-invariant) --
+    const size_t gps = plane_bytes(d.g), xps = plane_bytes(d.x);
+    const int grow = d.g.wp * 32, xrow = d.x.wp * 32;
+    const int cs4 = d.cout >> 2;
+    uint32_t off[C::IPW];
+#pragma unroll
+    for (int k = 0; k < C::IPW; ++k) {
+        const int j = wave + C::WM * k;
+        uint32_t o = 0;
+        if (j < C::G_INSTR) {
+            const int pl = j / C::G_IPL, rr = j - pl * C::G_IPL;
+            const int ch = cot * C::CO_T + pl * 16;
+            if (d.g_sub2) {  // kernel channel ch = s*cout/4 + c  →  G pixel (2y + (s>>1), 2x + (s&1)), channel c
+                const int sp = ch / cs4, c = ch - sp * cs4;
+                o = (uint32_t)((size_t)(c >> 4) * gps + (size_t)(2 * rr + (sp >> 1)) * grow + (sp & 1) * 32 +
+                               (lane >> 1) * 64 + (lane & 1) * 16);
+            } else {
+                o = (uint32_t)((size_t)(ch >> 4) * gps + (size_t)rr * grow + lane * 16);
+            }
+        } else if (j < C::INSTR) {
+            const int jx = j - C::G_INSTR;
+            const int pl = jx / C::X_IPL, jj = jx - pl * C::X_IPL;
+            const int u = jj * 64 + lane;
+            int q = u >> 1;
+            if (q >= C::XPIX) q = 0;  // tail lanes of the last instruction: harmless duplicate
+            const int row = q / 34, col = q - row * 34;
+            o = (uint32_t)((size_t)((cit * C::CI_T) / 16 + pl) * xps + (size_t)row * xrow + col * 32 + (u & 1) * 16);
+        }
+        off[k] = o;
+    }
+    auto lds_dst = [&](int j) -> int {
+        if (j < C::G_INSTR) {
+            const int pl = j / C::G_IPL, rr = j - pl * C::G_IPL;
+            return pl * C::G_PLANE + rr * 1024;
+        }
+        const int jx = j - C::G_INSTR;
+        const int pl = jx / C::X_IPL, jj = jx - pl * C::X_IPL;
+        return C::G_BYTES + pl * C::X_PLANE + jj * 1024;
+    };
+    auto stage = [&](int t, int buf) {
+        const int bx = t % nbx;
+        int r = t / nbx;
+        const int by = r % nby, img = r / nby;
+        const int x0 = bx * 32, y0 = by * TY;
+        // view_at with channel 0: the per-lane offsets carry the plane / sub-position
+        const char* gb = d.g_sub2 ? view_at(d.g, img, 2 * y0, 2 * x0, 0) : view_at(d.g, img, y0, x0, 0);
+        const char* xb = view_at(d.x, img, y0 - 1, x0 - 1, 0);
+        char* dst = smem + buf * C::STAGE;
+#pragma unroll
+        for (int k = 0; k < C::IPW; ++k) {
+            const int j = wave + C::WM * k;
+            if (j < C::INSTR) glds16((j < C::G_INSTR ? gb : xb) + off[k], dst + lds_dst(j));
+        }
+    };
+
+    f32x16 acc[3][NCO][NCI];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int f = 0; f < NCO; ++f)
+#pragma unroll
+            for (int e = 0; e < NCI; ++e)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) acc[dx][f][e][g] = 0.f;
+    float bsum[NCO];
+#pragma unroll
+    for (int f = 0; f < NCO; ++f) bsum[f] = 0.f;
+    const bool do_bias = d.db && cit == 0 && wave == 1;
+
+    // transposed-read lane geometry: plane gi of the 32-channel fragment, pixel q + 8h, channels 4p..4p+3
+    const int gi = (lane >> 4) & 1, hh = lane >> 5, q = (lane >> 2) & 3, p = lane & 3;
+    const int a_lane = gi * C::G_PLANE + (8 * hh + q) * 32 + 8 * p;
+    const int b_lane = C::G_BYTES + gi * C::X_PLANE + (8 * hh + q) * 32 + 8 * p;
+
+    if (t0 < t1) stage(t0, 0);
+    for (int t = t0; t < t1; ++t) {
+        const int cur = (t - t0) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (t + 1 < t1) stage(t + 1, cur ^ 1);
+        const char* base = smem + cur * C::STAGE;
+#pragma unroll
+        for (int kg = 0; kg < 2 * TY; ++kg) {
+            const int r = kg >> 1, c0 = (kg & 1) * 16;
+            bf16x8 fa[NCO];
+#pragma unroll
+            for (int f = 0; f < NCO; ++f) {
+                const char* pa = base + a_lane + 2 * f * C::G_PLANE + (r * 32 + c0) * 32;
+                fa[f] = cat4(lds_tr4(pa), lds_tr4(pa + 4 * 32));
+            }
+            if (do_bias) {
+#pragma unroll
+                for (int f = 0; f < NCO; ++f)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bsum[f] += (float)fa[f][e];
+            }
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                bf16x8 fb[NCI];
+#pragma unroll
+                for (int e = 0; e < NCI; ++e) {
+                    const char* pb = base + b_lane + 2 * e * C::X_PLANE + ((r + wave) * 34 + c0 + dx) * 32;
+                    fb[e] = cat4(lds_tr4(pb), lds_tr4(pb + 4 * 32));
+                }
+#pragma unroll
+                for (int f = 0; f < NCO; ++f)
+#pragma unroll
+                    for (int e = 0; e < NCI; ++e) acc[dx][f][e] = mfma32(fa[f], fb[e], acc[dx][f][e]);
+            }
+        }
+    }
+
+    // ---- partial sums: ws[split][tap][co][ci], D[co = (g&3)+8(g>>2)+4h][ci = l31]
+    const int l31 = lane & 31;
+    float* wsp = a.ws + (size_t)split * 9 * d.cout * d.cin;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+        float* wt = wsp + (size_t)(wave * 3 + dx) * d.cout * d.cin;
+#pragma unroll
+        for (int f = 0; f < NCO; ++f)
+#pragma unroll
+            for (int e = 0; e < NCI; ++e)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int co = cot * C::CO_T + f * 32 + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                    const int ci = cit * C::CI_T + e * 32 + l31;
+                    wt[(size_t)co * d.cin + ci] = acc[dx][f][e][g];
+                }
+    }
+    if (d.db && cit == 0 && wave == 1) {
+        float* bp = a.ws + (size_t)a.splits * 9 * d.cout * d.cin + (size_t)split * d.cout;
+#pragma unroll
+        for (int f = 0; f < NCO; ++f) {
+            const float v = bsum[f] + __shfl_xor(bsum[f], 32);
+            if (hh == 0) bp[cot * C::CO_T + f * 32 + (gi * 16 + (lane & 15))] = v;
+        }
+    }
+}
+
+// dW[co][ci][tap] (reference OIHW) = scale * sum_s ws[s][tap][co'][ci];  co' = kernel channel order.
+__global__ void wgrad_reduce_kernel(WgradArgs a) {
+    const isr_wgrad_desc& d = a.d;
+    const size_t per = (size_t)9 * d.cout * d.cin;
+    const int cs4 = d.cout >> 2;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < per + d.cout;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        if (idx < per) {
+            const int ci = (int)(idx % d.cin);
+            const int cok = (int)((idx / d.cin) % d.cout);
+            const int tap = (int)(idx / ((size_t)d.cin * d.cout));
+            float s = 0.f;
+            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[sp * per + idx];
+            const int co = d.g_sub2 ? (cok % cs4) * 4 + cok / cs4 : cok;
+            d.dw[((size_t)co * d.cin + ci) * 9 + tap] = s * d.scale;
+        } else if (d.db) {
+            const int cok = (int)(idx - per);
+            float s = 0.f;
+            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[(size_t)a.splits * per + (size_t)sp * d.cout + cok];
+            const int co = d.g_sub2 ? (cok % cs4) * 4 + cok / cs4 : cok;
+            d.db[co] = s * d.scale;
+        }
+    }
+}
+
+using WG22 = WG<2, 2, 2>;
+using WG12 = WG<1, 2, 2>;
+using WG21 = WG<2, 1, 2>;
+using WG11 = WG<1, 1, 2>;
+
+static int wgrad_splits(const isr_wgrad_desc* d, int tiles, int pairs) {
+    if (d->splits > 0) return d->splits < tiles ? d->splits : tiles;
+    int s = (640 + pairs - 1) / pairs;
+    return s < tiles ? s : tiles;
+}
+
+template <class C>
+static void wgrad_geometry(const isr_wgrad_desc* d, int* tiles, int* splits) {
+    *tiles = d->n * (d->ha / C::TY) * (d->wa / 32);
+    *splits = wgrad_splits(d, *tiles, (d->cout / C::CO_T) * (d->cin / C::CI_T));
+}
+
+template <class C>
+static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s) {
+    WgradArgs a;
+    a.d = *d;
+    wgrad_geometry<C>(d, &a.tiles, &a.splits);
+    if (ws_bytes < ((size_t)a.splits * 9 * d->cout * d->cin + (size_t)a.splits * d->cout) * 4) return -3;
+    a.ws = (float*)ws;
+    auto kern = wgrad3x3_kernel<C>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+        attr = true;
+    }
+    const int blocks = a.splits * (d->cout / C::CO_T) * (d->cin / C::CI_T);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, a);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(512), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <class F>
+static auto wgrad_pick(const isr_wgrad_desc* d, F&& f) {
+    const bool co2 = d->cout % 64 == 0, ci2 = d->cin % 64 == 0;
+    if (co2 && ci2) return f(WG22());
+    if (ci2) return f(WG12());
+    if (co2) return f(WG21());
+    return f(WG11());
+}
+
+size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d) {
+    return wgrad_pick(d, [&](auto c) {
+        using C = decltype(c);
+        int tiles, splits;
+        wgrad_geometry<C>(d, &tiles, &splits);
+        return ((size_t)splits * 9 * d->cout * d->cin + (size_t)splits * d->cout) * 4;
+    });
+}
+
+int wgrad3x3_dispatch(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s) {
+    return wgrad_pick(d, [&](auto c) { return launch_wgrad<decltype(c)>(d, ws, ws_bytes, s); });
+}
+
+}  // namespace isr

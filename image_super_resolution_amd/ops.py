@@ -12,7 +12,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._lib import IsrConvDesc, IsrHeadDesc, IsrTailDesc, IsrView, TILE_H, TILE_W, check
+from ._lib import IsrConvDesc, IsrHeadDesc, IsrTailDesc, IsrView, IsrWgrad9Desc, IsrWgradDesc, TILE_H, TILE_W, check
 
 
 def round_up(v: int, m: int) -> int:
@@ -112,6 +112,24 @@ def pack_conv3x3(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def pack_conv3x3_dgrad(w: torch.Tensor, scale: float = 1.0, sub2: bool = False,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """Layer weights [cout, cin, 3, 3] → packed weights of the input-gradient conv
+    cout → cin (180°-rotated, times `scale`; `sub2` = PixelShuffle channel order)."""
+    _require_gpu(w, "pack_conv3x3_dgrad")
+    lib = _lib.load()
+    cout, cin = w.shape[:2]
+    w = w.detach().float().contiguous()
+    n = lib.isr_conv3x3_packed_bytes(cin, cout) // 2
+    if out is None:
+        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    elif out.numel() != n or out.dtype != torch.bfloat16:
+        raise ValueError("pack_conv3x3_dgrad: bad output buffer")
+    check(lib.isr_pack_conv3x3_dgrad(w.data_ptr(), out.data_ptr(), cout, cin, scale, int(sub2), _stream()),
+          "isr_pack_conv3x3_dgrad")
+    return out
+
+
 def pack_head9x9(w: torch.Tensor) -> torch.Tensor:
     _require_gpu(w, "pack_head9x9")
     lib = _lib.load()
@@ -175,7 +193,8 @@ def conv3x3(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor | No
 
 def head9x9_desc(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor | None, y: ActBuffer, *,
                  slope: float, y2: ActBuffer | None = None, y2_coff: int = 0,
-                 mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)) -> IsrHeadDesc:
+                 mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225),
+                 m: ActBuffer | None = None, mslope: float = 1.0) -> IsrHeadDesc:
     _require_gpu(x, "head9x9")
     if not x.is_contiguous():
         raise ValueError("head9x9: input must be contiguous NCHW")
@@ -197,6 +216,8 @@ def head9x9_desc(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor | None
     d.wpack = wpack.data_ptr()
     d.bias = bias.data_ptr() if bias is not None else None
     d.slope = slope
+    d.m = m.view(0) if m is not None else _NULL_VIEW
+    d.mslope = mslope
     return d
 
 
@@ -233,3 +254,92 @@ def launch_tail9x9(d: IsrTailDesc) -> None:
 def tail9x9(x: ActBuffer, wpack: torch.Tensor, bias: torch.Tensor | None, out: torch.Tensor) -> None:
     """out (NCHW [n,3,h,w], fp32 or uint8) = tanh(conv9x9(x) + bias) (→ uint8 image)."""
     launch_tail9x9(tail9x9_desc(x, wpack, bias, out))
+
+
+# ---------------------------------------------------------------- backward
+class Workspace:
+    """Grow-only device scratch for split-K partial sums (the library never allocates)."""
+
+    def __init__(self):
+        self.t = None
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        if self.t is None or self.t.numel() < nbytes or self.t.device != torch.device(device):
+            self.t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        return self.t
+
+
+_WS = Workspace()
+
+
+def wgrad3x3_desc(x: ActBuffer, cin: int, g: ActBuffer, cout: int, dw: torch.Tensor, db: torch.Tensor | None = None,
+                  *, x_coff: int = 0, g_coff: int = 0, scale: float = 1.0, g_sub2: bool = False,
+                  splits: int = 0) -> IsrWgradDesc:
+    """dw[cout, cin, 3, 3] = scale * sum g ⊗ shifted x (fp32, overwritten); db[cout] likewise."""
+    if dw.dtype != torch.float32 or not dw.is_contiguous() or tuple(dw.shape) != (cout, cin, 3, 3):
+        raise ValueError("wgrad3x3: dw must be contiguous fp32 [cout, cin, 3, 3]")
+    if db is not None and (db.dtype != torch.float32 or not db.is_contiguous() or db.numel() != cout):
+        raise ValueError("wgrad3x3: db must be contiguous fp32 [cout]")
+    d = IsrWgradDesc()
+    d.n, d.h, d.w, d.ha, d.wa = x.n, x.h, x.w, x.ha, x.wa
+    d.cin, d.cout = cin, cout
+    d.x = x.view(x_coff)
+    d.g = g.view(g_coff)
+    d.g_sub2 = int(bool(g_sub2))
+    d.scale = scale
+    d.dw = dw.data_ptr()
+    d.db = db.data_ptr() if db is not None else None
+    d.splits = splits
+    return d
+
+
+def launch_wgrad3x3(d: IsrWgradDesc, device) -> None:
+    lib = _lib.load()
+    nbytes = lib.isr_wgrad3x3_workspace_bytes(ctypes.byref(d))
+    if nbytes == 0:
+        check(lib.isr_wgrad3x3(ctypes.byref(d), None, 0, _stream()), "isr_wgrad3x3")
+    ws = _WS.get(nbytes, device)
+    check(lib.isr_wgrad3x3(ctypes.byref(d), ws.data_ptr(), ws.numel(), _stream()), "isr_wgrad3x3")
+
+
+def wgrad3x3(x: ActBuffer, cin: int, g: ActBuffer, cout: int, dw: torch.Tensor, db: torch.Tensor | None = None,
+             **kw) -> None:
+    launch_wgrad3x3(wgrad3x3_desc(x, cin, g, cout, dw, db, **kw), x.t.device)
+
+
+def wgrad9x9_desc(p: torch.Tensor, q: ActBuffer, dw: torch.Tensor, db: torch.Tensor | None = None, *, head: bool,
+                  scale: float = 1.0, splits: int = 0) -> IsrWgrad9Desc:
+    """9x9 conv weight gradient (see include/isr.h isr_wgrad9_desc)."""
+    _require_gpu(p, "wgrad9x9")
+    if p.dtype != torch.float32 or not p.is_contiguous() or p.dim() != 4 or p.shape[1] != 3:
+        raise ValueError("wgrad9x9: p must be contiguous fp32 [n, 3, h, w]")
+    shape = (64, 3, 9, 9) if head else (3, 64, 9, 9)
+    if dw.dtype != torch.float32 or not dw.is_contiguous() or tuple(dw.shape) != shape:
+        raise ValueError(f"wgrad9x9: dw must be contiguous fp32 {shape}")
+    if db is not None and (db.dtype != torch.float32 or not db.is_contiguous() or db.numel() != shape[0]):
+        raise ValueError("wgrad9x9: bad db")
+    if tuple(p.shape[2:]) != (q.h, q.w) or p.shape[0] != q.n:
+        raise ValueError("wgrad9x9: p / q grids differ")
+    d = IsrWgrad9Desc()
+    d.n, d.h, d.w, d.ha, d.wa = q.n, q.h, q.w, q.ha, q.wa
+    d.head = int(bool(head))
+    d.p = p.data_ptr()
+    d.q = q.view(0)
+    d.scale = scale
+    d.dw = dw.data_ptr()
+    d.db = db.data_ptr() if db is not None else None
+    d.splits = splits
+    return d
+
+
+def launch_wgrad9x9(d: IsrWgrad9Desc, device) -> None:
+    lib = _lib.load()
+    nbytes = lib.isr_wgrad9x9_workspace_bytes(ctypes.byref(d))
+    if nbytes == 0:
+        check(lib.isr_wgrad9x9(ctypes.byref(d), None, 0, _stream()), "isr_wgrad9x9")
+    ws = _WS.get(nbytes, device)
+    check(lib.isr_wgrad9x9(ctypes.byref(d), ws.data_ptr(), ws.numel(), _stream()), "isr_wgrad9x9")
+
+
+def wgrad9x9(p: torch.Tensor, q: ActBuffer, dw: torch.Tensor, db: torch.Tensor | None = None, **kw) -> None:
+    launch_wgrad9x9(wgrad9x9_desc(p, q, dw, db, **kw), p.device)

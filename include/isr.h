@@ -101,6 +101,12 @@ typedef struct isr_head_desc {
     const void* wpack;     /* from isr_pack_head9x9 */
     const float* bias;     /* [cout] or NULL */
     float slope;
+    /* backward use (zero in the forward): with fp32 input, mean 0, inv_std 1,
+     * slope 1 and 180°-rotated, transposed weights this is the input gradient of
+     * the 9x9 tail conv (utils/models.py:607, :636); m masks it with
+     * LeakyReLU'(m) of slope mslope (the last Scaler's activation). */
+    isr_view m;
+    float mslope;
 } isr_head_desc;
 
 /* 9x9 tail conv, cin (=64) → 3 channels, + bias + tanh, NCHW out (fp32, or
@@ -117,11 +123,64 @@ typedef struct isr_tail_desc {
     int32_t y_u8;            /* 0: fp32 tanh output; 1: uint8 image */
 } isr_tail_desc;
 
+/* Weight / bias gradient of a 3x3 'same' conv (the bwd-weight half of autograd
+ * through Conv / ConvWithoutBN / RDB / Scaler, utils/models.py:75-111, 174-199,
+ * 245-271, 572-589, driven by train.py:57 / :102):
+ *   dw[co][ci][ky][kx] = scale * sum_{n,y,x} g[n][co][y][x] * x[n][ci][y+ky-1][x+kx-1]
+ *   db[co]             = scale * sum_{n,y,x} g[n][co][y][x]
+ * g must be zero outside the valid h x w region (every isr kernel writes zeros there).
+ * Needs a caller-owned workspace of isr_wgrad3x3_workspace_bytes(desc) bytes
+ * (split-K partial sums); dw / db are overwritten. */
+typedef struct isr_wgrad_desc {
+    int32_t n, h, w, ha, wa; /* conv output grid (= input grid) */
+    int32_t cin, cout;       /* multiples of 32 */
+    isr_view x;              /* forward input, cin channels, pad >= 1 */
+    isr_view g;              /* gradient w.r.t. the conv output, cout channels */
+    int32_t g_sub2;          /* 1: g is the PixelShuffle(2)'d gradient on the 2h x 2w grid with cout/4
+                                channels (Scaler, utils/models.py:583); cout % 128 == 0 */
+    float scale;
+    float* dw;               /* [cout][cin][3][3] fp32 */
+    float* db;               /* [cout] fp32 or NULL */
+    int32_t splits;          /* split-K count; 0 = library choice */
+} isr_wgrad_desc;
+
+/* Weight / bias gradients of the 9x9 convs (same workspace contract):
+ *   head = 1: conv0 3 → 64 (utils/models.py:596, :625): p = the (normalised)
+ *             network input, q = gradient wrt conv0's pre-activation output;
+ *             dw [64][3][9][9], db [64].
+ *   head = 0: conv2 64 → 3 (utils/models.py:607, :636): p = gradient wrt
+ *             conv2's pre-tanh output, q = conv2's input (pad >= 4);
+ *             dw [3][64][9][9], db [3].
+ * dw[co][ci][ky][kx] = scale * sum_{n,y,x} gout[co][y][x] * in[ci][y+ky-4][x+kx-4]. */
+typedef struct isr_wgrad9_desc {
+    int32_t n, h, w, ha, wa;
+    int32_t head;
+    const float* p;          /* NCHW fp32 [n][3][h][w] */
+    isr_view q;              /* 64 channels, zero outside h x w */
+    float scale;
+    float* dw;
+    float* db;               /* or NULL */
+    int32_t splits;          /* 0 = library choice */
+} isr_wgrad9_desc;
+
+size_t isr_wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
+int isr_wgrad9x9(const isr_wgrad9_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
+
+size_t isr_wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
+int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
+
 /* Weight packing (device fp32 OIHW → device bf16 kernel layout).  Replaces the
  * one-off fuse step's weight preparation (utils/models.py:741-751); BN folding
  * itself is done by the caller before packing. */
 size_t isr_conv3x3_packed_bytes(int32_t cout, int32_t cin);
 int isr_pack_conv3x3(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
+/* Input-gradient (dgrad) packing of a layer's [cout][cin][3][3] weights: the
+ * result is an isr_conv3x3_fwd weight set for the conv cout → cin with the
+ * kernel rotated by 180° and multiplied by `scale` (isr_conv3x3_packed_bytes(cin,
+ * cout) bytes).  sub2 = 1 orders its input channels for isr_conv_desc.x_sub2
+ * (the Scaler backward, utils/models.py:583). */
+int isr_pack_conv3x3_dgrad(const float* w_oihw, void* packed, int32_t cout, int32_t cin, float scale, int32_t sub2,
+                           isr_stream_t s);
 size_t isr_head9x9_packed_bytes(int32_t cout, int32_t cin);
 int isr_pack_head9x9(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
 size_t isr_tail9x9_packed_bytes(int32_t cout, int32_t cin);

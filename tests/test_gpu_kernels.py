@@ -226,3 +226,144 @@ def test_conv3x3_x_sub2_is_pixel_unshuffle(h, w):
     torch.cuda.synchronize()
     ref = F.conv2d(F.pixel_unshuffle(bf(g), 2), bf(Wu), padding=1)
     close(lr.to_nchw(), ref)
+
+
+def _wgrad_ref(x, g, scale=1.0):
+    """autograd reference: dW, db of y = conv2d(x, W, b, padding=1) for upstream grad g."""
+    cin, cout = x.shape[1], g.shape[1]
+    W = torch.zeros(cout, cin, 3, 3, device=DEV, requires_grad=True)
+    b = torch.zeros(cout, device=DEV, requires_grad=True)
+    y = F.conv2d(x, W, b, padding=1)
+    y.backward(g)
+    return W.grad * scale, b.grad * scale
+
+
+def _close_rel(got, ref, tol=2e-2):
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < tol, f"relative L2 error {rel:.3e}"
+    lim = tol * ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= lim * 2, f"max err {(got - ref).abs().max().item():.3e}"
+
+
+@pytest.mark.parametrize("n,cin,cout,h,w,splits", [(2, 64, 32, 20, 36, 0), (1, 96, 32, 33, 65, 0),
+                                                   (2, 192, 64, 18, 40, 0), (1, 64, 64, 7, 5, 3),
+                                                   (2, 32, 160, 16, 32, 0), (1, 64, 192, 24, 24, 1)])
+def test_wgrad3x3(n, cin, cout, h, w, splits):
+    from image_super_resolution_amd import ops
+    x = bf(_mk(n, cin, h, w, 51))
+    g = bf(_mk(n, cout, h, w, 52))
+    xb = ops.ActBuffer.from_nchw(x, pad=1)
+    gb = ops.ActBuffer.from_nchw(g, pad=1)
+    dw = torch.empty(cout, cin, 3, 3, device=DEV)
+    db = torch.empty(cout, device=DEV)
+    ops.wgrad3x3(xb, cin, gb, cout, dw, db, scale=0.5, splits=splits)
+    torch.cuda.synchronize()
+    rw, rb = _wgrad_ref(x, g, 0.5)
+    _close_rel(dw, rw, 1e-3)
+    _close_rel(db, rb, 1e-3)
+
+
+def test_wgrad3x3_dense_slices_and_sub2():
+    """wgrad reading channel slices of a dense buffer, and the Scaler's
+    PixelShuffle'd gradient (g_sub2) with reference channel order."""
+    from image_super_resolution_amd import ops
+    n, h, w = 2, 20, 24
+    dense = _mk(n, 192, h, w, 61)
+    db_ = ops.ActBuffer.from_nchw(dense, pad=1)
+    dw = torch.empty(32, 128, 3, 3, device=DEV)
+    ops.wgrad3x3(db_, 128, db_, 32, dw, None, g_coff=160)
+    torch.cuda.synchronize()
+    rw, _ = _wgrad_ref(bf(dense)[:, :128], bf(dense)[:, 160:192])
+    _close_rel(dw, rw, 1e-3)
+    # Scaler: y = shuffle(conv(x)); grad wrt conv output = pixel_unshuffle(g_hr)
+    x = bf(_mk(n, 64, h, w, 62))
+    ghr = bf(_mk(n, 64, 2 * h, 2 * w, 63))
+    xb = ops.ActBuffer.from_nchw(x, pad=1)
+    gb = ops.ActBuffer.alloc(n, 2 * h, 2 * w, 64, 2, DEV, ha=2 * xb.ha, wa=2 * xb.wa)
+    gb.set_nchw(ghr, 0)
+    dw = torch.empty(256, 64, 3, 3, device=DEV)
+    dbias = torch.empty(256, device=DEV)
+    ops.wgrad3x3(xb, 64, gb, 256, dw, dbias, g_sub2=True)
+    torch.cuda.synchronize()
+    rw, rb = _wgrad_ref(x, F.pixel_unshuffle(ghr, 2))
+    _close_rel(dw, rw, 1e-3)
+    _close_rel(dbias, rb, 1e-3)
+
+
+def test_dgrad_via_transposed_pack():
+    """Input gradient = conv3x3 with the dgrad-packed weights (incl. scale and the
+    Scaler's x_sub2 order) vs autograd."""
+    from image_super_resolution_amd import ops
+    n, h, w = 2, 20, 36
+    for cin, cout, sub2 in [(64, 32, False), (32, 160, False), (192, 64, False), (64, 256, True)]:
+        x = _mk(n, cin, h, w, 71).requires_grad_(True)
+        W = _w(cout, cin, 3, 72)
+        y = F.conv2d(x, bf(W), padding=1)
+        gy = bf(_mk(n, cout, h, w, 73))
+        if sub2:
+            ghr = bf(_mk(n, cout // 4, 2 * h, 2 * w, 74))
+            gy = F.pixel_unshuffle(ghr, 2)
+        y.backward(gy)
+        wp = ops.pack_conv3x3_dgrad(W, scale=0.25, sub2=sub2)
+        out = ops.ActBuffer.alloc(n, h, w, cin, 1, DEV)
+        if sub2:
+            gb = ops.ActBuffer.alloc(n, 2 * h, 2 * w, cout // 4, 2, DEV, ha=2 * out.ha, wa=2 * out.wa)
+            gb.set_nchw(ghr, 0)
+        else:
+            gb = ops.ActBuffer.from_nchw(gy, pad=1)
+        ops.conv3x3(gb, cout, wp, None, cin, out, x_sub2=sub2)
+        torch.cuda.synchronize()
+        close(out.to_nchw(), x.grad * 0.25)
+
+
+def _wgrad9_ref(inp, gout, cin, cout):
+    W = torch.zeros(cout, cin, 9, 9, device=DEV, requires_grad=True)
+    b = torch.zeros(cout, device=DEV, requires_grad=True)
+    F.conv2d(inp, W, b, padding=4).backward(gout)
+    return W.grad, b.grad
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 20, 36), (1, 64, 64), (3, 7, 70)])
+def test_wgrad9x9_tail_and_head(n, h, w):
+    from image_super_resolution_amd import ops
+    # tail conv2: 64 → 3 on the HR grid
+    U = bf(_mk(n, 64, h, w, 81))
+    gp = bf(_mk(n, 3, h, w, 82))
+    ub = ops.ActBuffer.from_nchw(U, pad=4)
+    dw = torch.empty(3, 64, 9, 9, device=DEV)
+    db = torch.empty(3, device=DEV)
+    ops.wgrad9x9(gp.contiguous(), ub, dw, db, head=False, scale=2.0)
+    torch.cuda.synchronize()
+    rw, rb = _wgrad9_ref(U, gp, 64, 3)
+    _close_rel(dw, rw * 2, 1e-3)
+    _close_rel(db, rb * 2, 1e-3)
+    # head conv0: 3 → 64 on the LR grid
+    X = bf(_mk(n, 3, h, w, 83))
+    gq = bf(_mk(n, 64, h, w, 84))
+    qb = ops.ActBuffer.from_nchw(gq, pad=1)
+    dw = torch.empty(64, 3, 9, 9, device=DEV)
+    db = torch.empty(64, device=DEV)
+    ops.wgrad9x9(X.contiguous(), qb, dw, db, head=True)
+    torch.cuda.synchronize()
+    rw, rb = _wgrad9_ref(X, gq, 3, 64)
+    _close_rel(dw, rw, 1e-3)
+    _close_rel(db, rb, 1e-3)
+
+
+def test_tail_dgrad_via_head_kernel_with_mask():
+    """Input gradient of the 9x9 tail conv (64 → 3) = head kernel with rotated,
+    transposed weights, masked by LeakyReLU'(last Scaler output)."""
+    from image_super_resolution_amd import ops
+    n, h, w = 2, 40, 72
+    U = _mk(n, 64, h, w, 91).requires_grad_(True)
+    W2 = _w(3, 64, 9, 92)
+    gp = bf(_mk(n, 3, h, w, 93))
+    F.conv2d(U, bf(W2), padding=4).backward(gp)
+    act = _mk(n, 64, h, w, 94)
+    mb = ops.ActBuffer.from_nchw(act, pad=1)
+    Wt = W2.flip(2, 3).transpose(0, 1).contiguous()  # [64][3][9][9]
+    out = ops.ActBuffer.alloc(n, h, w, 64, 2, DEV)
+    ops.head9x9(gp.contiguous(), ops.pack_head9x9(Wt), None, out, slope=1.0, m=mb, mslope=0.01)
+    torch.cuda.synchronize()
+    ref = U.grad * torch.where(bf(act) > 0, 1.0, 0.01)
+    close(out.to_nchw(), ref)
