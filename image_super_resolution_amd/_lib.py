@@ -57,6 +57,12 @@ class IsrWgrad9Desc(ctypes.Structure):
                 ("dw", c_void_p), ("db", c_void_p), ("splits", c_int32)]
 
 
+class IsrEwDesc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32), ("c", c_int32),
+                ("y", IsrView), ("a", IsrView), ("b", IsrView), ("m", IsrView),
+                ("sa", c_float), ("sb", c_float), ("mslope", c_float)]
+
+
 # Every symbol include/isr.h declares, with its ctypes signature.
 SIGNATURES = {
     "isr_conv3x3_packed_bytes": (c_size_t, [c_int32, c_int32]),
@@ -66,6 +72,7 @@ SIGNATURES = {
     "isr_wgrad3x3": (c_int32, [POINTER(IsrWgradDesc), c_void_p, c_size_t, c_void_p]),
     "isr_wgrad9x9_workspace_bytes": (c_size_t, [POINTER(IsrWgrad9Desc)]),
     "isr_wgrad9x9": (c_int32, [POINTER(IsrWgrad9Desc), c_void_p, c_size_t, c_void_p]),
+    "isr_ew_combine": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
     "isr_head9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),
     "isr_pack_head9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "isr_tail9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),

@@ -19,6 +19,7 @@ size_t tail9x9_packed_bytes();
 int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale, int sub2, hipStream_t s);
+int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s);
 size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
 size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
 int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
@@ -240,6 +241,18 @@ int isr_wgrad9x9(const isr_wgrad9_desc* d, void* workspace, size_t ws_bytes, isr
     rc = isr::wgrad9x9_dispatch(d, workspace, ws_bytes, (hipStream_t)s);
     if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad9x9: workspace too small");
     return launched(rc, "wgrad9x9");
+}
+
+int isr_ew_combine(const isr_ew_desc* d, isr_stream_t s) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "ew_combine: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0 || d->c % 16)
+        return fail(ISR_ERR_BAD_DESC, "ew_combine: bad problem n=%d h=%d w=%d c=%d", d->n, d->h, d->w, d->c);
+    if (d->ha < d->h || d->wa < d->w) return fail(ISR_ERR_BAD_DESC, "ew_combine: computed region smaller than valid");
+    if (!view_ok(d->y, d->ha, d->wa, 0, d->c, "ew.y", 1) || !view_ok(d->a, d->ha, d->wa, 0, d->c, "ew.a", 1))
+        return ISR_ERR_BAD_DESC;
+    if (d->b.data && !view_ok(d->b, d->ha, d->wa, 0, d->c, "ew.b", 1)) return ISR_ERR_BAD_DESC;
+    if (d->m.data && !view_ok(d->m, d->ha, d->wa, 0, d->c, "ew.m", 1)) return ISR_ERR_BAD_DESC;
+    return launched(isr::ew_combine_dispatch(d, (hipStream_t)s), "ew_combine");
 }
 
 }  // extern "C"

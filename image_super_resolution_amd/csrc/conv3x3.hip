@@ -131,6 +131,7 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
                 const int cf = ct * CT + f * 32;
                 const bool use_r1 = (MODE & 1) && (d.r1_cn == 0 || cf < d.r1_cn);
                 const bool use_m = (MODE & 16) && cf >= d.m_c0;
+                const bool scale2 = d.s2 != 1.f;  // s2 also scales when there is no r2 (backward)
 #pragma unroll
                 for (int blk = 0; blk < 2; ++blk) {
                     const int co = cf + 16 * blk + 8 * hh;
@@ -158,7 +159,11 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
                     for (int e = 0; e < 8; ++e) {
                         u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
                         if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (use_r1 ? (float)q1[blk][e] : 0.f);
-                        if constexpr (MODE & 2) u[e] = u[e] * d.s2 + (float)q2[blk][e];
+                        if constexpr (MODE & 2) {
+                            u[e] = u[e] * d.s2 + (float)q2[blk][e];
+                        } else {
+                            if (scale2) u[e] *= d.s2;
+                        }
                         if constexpr (MODE & 16) {
                             if (use_m && !((float)qm[blk][e] > 0.f)) u[e] *= d.mslope;
                         }

@@ -208,7 +208,11 @@ class _Generator(nn.Module):
 
     def forward(self, inputs: torch.Tensor) -> torch.Tensor:
         _require_cuda(inputs, type(self).__name__)
-        _no_train(self, type(self).__name__)
+        if self.training and torch.is_grad_enabled():
+            # differentiable HIP path (forward saves every dense block; backward = libisr
+            # dgrad / wgrad kernels), train.py:52-63 / :88-102
+            from .train_engine import train_forward
+            return train_forward(self, inputs)
         return engine.run_generator(self._packed(inputs.device), inputs.float())
 
 

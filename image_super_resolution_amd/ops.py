@@ -12,7 +12,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._lib import IsrConvDesc, IsrHeadDesc, IsrTailDesc, IsrView, IsrWgrad9Desc, IsrWgradDesc, TILE_H, TILE_W, check
+from ._lib import IsrConvDesc, IsrEwDesc, IsrHeadDesc, IsrTailDesc, IsrView, IsrWgrad9Desc, IsrWgradDesc, TILE_H, TILE_W, check
 
 
 def round_up(v: int, m: int) -> int:
@@ -101,13 +101,17 @@ _NULL_VIEW = IsrView(None, 0, 0, 0, 0, 0)
 
 
 # ---------------------------------------------------------------- packing
-def pack_conv3x3(w: torch.Tensor) -> torch.Tensor:
+def pack_conv3x3(w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """fp32 OIHW [cout, cin, 3, 3] device weights → packed bf16 kernel layout."""
     _require_gpu(w, "pack_conv3x3")
     lib = _lib.load()
     cout, cin = w.shape[:2]
     w = w.detach().float().contiguous()
-    out = torch.empty(lib.isr_conv3x3_packed_bytes(cout, cin) // 2, dtype=torch.bfloat16, device=w.device)
+    n = lib.isr_conv3x3_packed_bytes(cout, cin) // 2
+    if out is None:
+        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    elif out.numel() != n or out.dtype != torch.bfloat16:
+        raise ValueError("pack_conv3x3: bad output buffer")
     check(lib.isr_pack_conv3x3(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_conv3x3")
     return out
 
@@ -130,22 +134,30 @@ def pack_conv3x3_dgrad(w: torch.Tensor, scale: float = 1.0, sub2: bool = False,
     return out
 
 
-def pack_head9x9(w: torch.Tensor) -> torch.Tensor:
+def pack_head9x9(w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _require_gpu(w, "pack_head9x9")
     lib = _lib.load()
     cout, cin = w.shape[:2]
     w = w.detach().float().contiguous()
-    out = torch.empty(lib.isr_head9x9_packed_bytes(cout, cin) // 2, dtype=torch.bfloat16, device=w.device)
+    n = lib.isr_head9x9_packed_bytes(cout, cin) // 2
+    if out is None:
+        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    elif out.numel() != n or out.dtype != torch.bfloat16:
+        raise ValueError("pack_head9x9: bad output buffer")
     check(lib.isr_pack_head9x9(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_head9x9")
     return out
 
 
-def pack_tail9x9(w: torch.Tensor) -> torch.Tensor:
+def pack_tail9x9(w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _require_gpu(w, "pack_tail9x9")
     lib = _lib.load()
     cout, cin = w.shape[:2]
     w = w.detach().float().contiguous()
-    out = torch.empty(lib.isr_tail9x9_packed_bytes(cout, cin) // 2, dtype=torch.bfloat16, device=w.device)
+    n = lib.isr_tail9x9_packed_bytes(cout, cin) // 2
+    if out is None:
+        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    elif out.numel() != n or out.dtype != torch.bfloat16:
+        raise ValueError("pack_tail9x9: bad output buffer")
     check(lib.isr_pack_tail9x9(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_tail9x9")
     return out
 
@@ -343,3 +355,20 @@ def launch_wgrad9x9(d: IsrWgrad9Desc, device) -> None:
 
 def wgrad9x9(p: torch.Tensor, q: ActBuffer, dw: torch.Tensor, db: torch.Tensor | None = None, **kw) -> None:
     launch_wgrad9x9(wgrad9x9_desc(p, q, dw, db, **kw), p.device)
+
+
+def ew_combine_desc(y: ActBuffer, a: ActBuffer, c: int, *, sa: float = 1.0, b: ActBuffer | None = None,
+                    sb: float = 1.0, m: ActBuffer | None = None, mslope: float = 1.0,
+                    y_coff: int = 0, a_coff: int = 0, b_coff: int = 0, m_coff: int = 0) -> IsrEwDesc:
+    """y = (a*sa + b*sb) * LeakyReLU'(m) over c channels (zero outside the valid region)."""
+    d = IsrEwDesc()
+    d.n, d.h, d.w, d.ha, d.wa, d.c = y.n, y.h, y.w, y.ha, y.wa, c
+    d.y, d.a = y.view(y_coff), a.view(a_coff)
+    d.b = b.view(b_coff) if b is not None else _NULL_VIEW
+    d.m = m.view(m_coff) if m is not None else _NULL_VIEW
+    d.sa, d.sb, d.mslope = sa, sb, mslope
+    return d
+
+
+def ew_combine(y: ActBuffer, a: ActBuffer, c: int, **kw) -> None:
+    check(_lib.load().isr_ew_combine(ctypes.byref(ew_combine_desc(y, a, c, **kw)), _stream()), "isr_ew_combine")

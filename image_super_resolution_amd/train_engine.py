@@ -1,0 +1,344 @@
+"""Training (forward + backward) of the RRDB generator on libisr (MI355X).
+
+Replaces autograd through EResNet / SRGAN(enchant) (utils/models.py:621-650,
+245-317, 572-589) as driven by train.py:52-63 and :88-102.  The forward keeps
+one 192-channel dense buffer per RDB (the block input in channels [0, 64) and
+the four growth outputs after it), so every activation the backward needs is
+resident and no concat is ever materialised.  The backward walks the network
+in reverse with three rotating 192-channel gradient buffers:
+
+  tail    wgrad9x9 (dW2, db2);  dgrad = head9x9 kernel with 180°-rotated W2ᵀ,
+          masked by LeakyReLU'(last Scaler output)
+  scalers wgrad3x3 reading the PixelShuffle'd gradient (g_sub2);  dgrad =
+          conv3x3 reading it as PixelShuffleᵀ (x_sub2) with LeakyReLU' mask
+  conv1   wgrad + dgrad into the last RRDB's output gradient
+  RRDB    per RDB (reverse): dgrad of the final conv writes the 192-channel
+          gradient [g_x0 + residual | g_slot1..4] with LeakyReLU' of slot 4;
+          growth conv k: wgrad, then dgrad accumulating into channels
+          [0, 64+32k) in place and masking slot k-1 — the cat-backward and
+          the activation backward are both epilogue work
+  trunk   g_f0 = chain + g_T, LeakyReLU'(f0) (ew_combine);  head wgrad9x9
+
+BatchNorm in train mode (ResNet) is not implemented on this path yet.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+from torch import nn
+
+from . import ops
+from ._lib import load as _load_lib
+from .ops import ActBuffer
+
+LEAKY = 0.01
+
+
+@dataclass
+class TConv:
+    """One conv layer of the generator: parameter references + packed copies."""
+    w: torch.Tensor
+    b: torch.Tensor | None
+    cin: int
+    cout: int
+    kind: str                  # "3x3", "head", "tail"
+    dgrad_scale: float = 1.0
+    sub2: bool = False         # dgrad reads the PixelShuffle'd gradient (Scaler)
+    fwd: torch.Tensor | None = None
+    bwd: torch.Tensor | None = None
+
+    def pack(self):
+        w = self.w.detach()
+        if self.kind == "3x3":
+            self.fwd = ops.pack_conv3x3(w, out=self.fwd)
+            self.bwd = ops.pack_conv3x3_dgrad(w, scale=self.dgrad_scale, sub2=self.sub2, out=self.bwd)
+        elif self.kind == "head":
+            self.fwd = ops.pack_head9x9(w, out=self.fwd)
+        else:  # tail: forward pack + its input-gradient conv run by the head kernel
+            self.fwd = ops.pack_tail9x9(w, out=self.fwd)
+            self.bwd = ops.pack_head9x9(w.float().flip(2, 3).transpose(0, 1).contiguous(), out=self.bwd)
+
+    @property
+    def bias(self) -> torch.Tensor:
+        return self.b.detach() if self.b is not None else None
+
+
+def _generator_convs(gen: nn.Module) -> tuple[TConv, list[list[TConv]], TConv, list[TConv], TConv]:
+    """Conv layers of an EResNet in execution order (reference module paths)."""
+    def t(conv: nn.Conv2d, kind="3x3", **kw):
+        return TConv(conv.weight, conv.bias, conv.in_channels, conv.out_channels, kind, **kw)
+
+    a = gen.add_rate
+    head = t(gen.conv0.conv, "head")
+    rdbs = []
+    for i, rrdb in enumerate(gen.residual):
+        for r, rdb in enumerate(rrdb.net):
+            # dgrad of the final conv carries the RDB (x add_rate) scale in the weights;
+            # the RRDB-level x add_rate of the third RDB is applied by the epilogue's s2
+            rdbs.append([t(rdb.conv0.conv), t(rdb.conv1.conv), t(rdb.conv2.conv), t(rdb.conv3.conv),
+                         t(rdb.conv.conv, dgrad_scale=a)])
+    conv1 = t(gen.conv1.conv)
+    scalers = [t(s.net[0].conv, sub2=True) for s in gen.scaler]
+    tail = t(gen.conv2.conv, "tail")
+    return head, rdbs, conv1, scalers, tail
+
+
+class GeneratorTrainPlan:
+    """Fixed-geometry training plan: buffers, packed weights and prebuilt
+    descriptors for one (n, h, w).  `forward(x)` / `backward(gy)`; parameter
+    gradients come back in the order of `params()`."""
+
+    def __init__(self, gen: nn.Module, n: int, h: int, w: int, device):
+        from .models import EResNet, SRGAN
+        if isinstance(gen, SRGAN):
+            gen = gen.res_net
+        if not isinstance(gen, EResNet):
+            raise NotImplementedError("HIP training path: EResNet / SRGAN(enchant=True) generators "
+                                      "(ResNet's train-mode BatchNorm is not implemented yet)")
+        self.gen, self.key = gen, (n, h, w, str(device))
+        self.device = torch.device(device)
+        self.a = float(gen.add_rate)
+        self.slope0 = float(gen.conv0.act.negative_slope)
+        self.head, self.rdbs, self.conv1, self.scalers, self.tail = _generator_convs(gen)
+        self.lib = _load_lib()
+        S = len(self.scalers)
+        dev = self.device
+        # ---- activations (saved for the backward)
+        self.f0 = ActBuffer.alloc(n, h, w, 64, 1, dev)
+        nr = len(self.rdbs)
+        self.D = [ActBuffer.alloc(n, h, w, 192, 1, dev) for _ in range(nr)] + [ActBuffer.alloc(n, h, w, 64, 1, dev)]
+        self.T = ActBuffer.alloc(n, h, w, 64, 1, dev)
+        self.ups = []
+        hh, ww, ha, wa = h, w, self.f0.ha, self.f0.wa
+        for s in range(S):
+            hh, ww, ha, wa = 2 * hh, 2 * ww, 2 * ha, 2 * wa
+            self.ups.append(ActBuffer.alloc(n, hh, ww, 64, 4 if s == S - 1 else 1, dev, ha=ha, wa=wa))
+        self.out_shape = (n, 3, hh, ww)
+        # ---- gradients
+        self.G = [ActBuffer.alloc(n, h, w, 192, 1, dev) for _ in range(3)]
+        self.gT = ActBuffer.alloc(n, h, w, 64, 1, dev)
+        self.gups = [ActBuffer.alloc(u.n, u.h, u.w, 64, 2, dev, ha=u.ha, wa=u.wa) for u in self.ups]
+        self.gf0 = ActBuffer.alloc(n, h, w, 64, 1, dev)
+        # ---- parameters / gradient layout (one flat fp32 gradient buffer per backward)
+        self.convs = [self.head] + [c for r in self.rdbs for c in r] + [self.conv1] + self.scalers + [self.tail]
+        self._params, self._goff = [], []
+        off = 0
+        for c in self.convs:
+            for p in (c.w, c.b):
+                if p is not None:
+                    self._params.append(p)
+                    self._goff.append(off)
+                    off += (p.numel() + 3) // 4 * 4  # 16-byte aligned views
+        self._gsize = off
+        self.pack()
+        self._build()
+
+    # ------------------------------------------------------------------ setup
+    def params(self) -> list[torch.Tensor]:
+        return list(self._params)
+
+    def pack(self) -> None:
+        """Refresh the packed bf16 weights from the fp32 parameters (every step)."""
+        for c in self.convs:
+            c.pack()
+
+    def _build(self):
+        a, lib = self.a, self.lib
+        conv, head, tail = lib.isr_conv3x3_fwd, lib.isr_head9x9_fwd, lib.isr_tail9x9_fwd
+        D, f0, T = self.D, self.f0, self.T
+        self.dummy_x = torch.empty(self.out_shape[0], 3, f0.h, f0.w, device=self.device)
+        self.dummy_y = torch.empty(self.out_shape, device=self.device)
+        F = []
+        self.head_desc = ops.head9x9_desc(self.dummy_x, self.head.fwd, self.head.bias, f0, slope=self.slope0, y2=D[0])
+        F.append((head, self.head_desc))
+        for j, cs in enumerate(self.rdbs):
+            for k in range(4):
+                c = cs[k]
+                F.append((conv, ops.conv3x3_desc(D[j], c.cin, c.fwd, c.bias, c.cout, D[j], y_coff=c.cin, slope=LEAKY)))
+            c = cs[4]
+            extra = dict(r2=D[j - 2], s2=a) if j % 3 == 2 else {}
+            F.append((conv, ops.conv3x3_desc(D[j], 192, c.fwd, c.bias, 64, D[j + 1], slope=1.0, r1=D[j], s1=a,
+                                             **extra)))
+        c = self.conv1
+        F.append((conv, ops.conv3x3_desc(D[-1], 64, c.fwd, c.bias, 64, T, slope=1.0, r1=f0, s1=1.0)))
+        cur = T
+        for s, c in enumerate(self.scalers):
+            F.append((conv, ops.conv3x3_desc(cur, 64, c.fwd, c.bias, 256, self.ups[s], slope=LEAKY, shuffle=2)))
+            cur = self.ups[s]
+        self.tail_desc = ops.tail9x9_desc(cur, self.tail.fwd, self.tail.bias, self.dummy_y)
+        F.append((tail, self.tail_desc))
+        self.fwd_launches = F
+
+        # ---- backward.  Entries: ("conv", desc) | ("wg3", desc, conv_index) | ("wg9", desc, conv_index)
+        #      | ("head", desc) | ("ew", desc).  dw/db pointers are patched per call.
+        B = []
+        ci = {id(c): i for i, c in enumerate(self.convs)}
+        dev = self.device
+
+        def wg3(x, cin, g, cout, c, *, x_coff=0, g_coff=0, scale=1.0, g_sub2=False):
+            d = ops.wgrad3x3_desc(x, cin, g, cout, _meta_dw(cout, cin, 3, dev), None, x_coff=x_coff, g_coff=g_coff,
+                                  scale=scale, g_sub2=g_sub2)
+            B.append(("wg3", d, ci[id(c)]))
+
+        # tail
+        self.gp = torch.empty(self.out_shape, device=dev)
+        ut = self.ups[-1]
+        d9 = ops.wgrad9x9_desc(self.gp, ut, _meta_dw(3, 64, 9, dev), None, head=False)
+        B.append(("wg9", d9, ci[id(self.tail)]))
+        B.append(("head", ops.head9x9_desc(self.gp, self.tail.bwd, None, self.gups[-1], slope=1.0, m=ut,
+                                           mslope=LEAKY)))
+        # scalers (reverse)
+        for s in range(len(self.scalers) - 1, -1, -1):
+            c = self.scalers[s]
+            xin = self.ups[s - 1] if s > 0 else T
+            wg3(xin, 64, self.gups[s], 256, c, g_sub2=True)
+            out = self.gups[s - 1] if s > 0 else self.gT
+            kw = dict(m=self.ups[s - 1], mslope=LEAKY) if s > 0 else {}
+            B.append(("conv", ops.conv3x3_desc(self.gups[s], 256, c.bwd, None, 64, out, x_sub2=True, **kw)))
+        # conv1:  T = conv1(D[-1][0:64]) + f0
+        c = self.conv1
+        U, V, W = self.G
+        wg3(D[-1], 64, self.gT, 64, c)
+        B.append(("conv", ops.conv3x3_desc(self.gT, 64, c.bwd, None, 64, U)))
+        # RRDBs, reverse
+        nb = len(self.rdbs) // 3
+        for i in range(nb - 1, -1, -1):
+            # g_R (gradient wrt the RRDB output) is in U[0:64]
+            seq = [(3 * i + 2, U, V), (3 * i + 1, V, W), (3 * i, W, V)]
+            for step, (j, gin, gout) in enumerate(seq):
+                cs = self.rdbs[j]
+                Dj = D[j]
+                c5 = cs[4]
+                last_rdb = step == 0  # the third RDB of the RRDB (first in reverse)
+                # final conv: out = conv*a + Dj[0:64]  (third RDB: (...)*a + RRDB input)
+                wg3(Dj, 192, gin, 64, c5, scale=(a * a if last_rdb else a))
+                B.append(("conv", ops.conv3x3_desc(gin, 64, c5.bwd, None, 192, gout, r1=gin, r1_cn=64,
+                                                   s2=(a if last_rdb else 1.0), m=Dj, m_c0=160, mslope=LEAKY)))
+                for k in range(3, -1, -1):
+                    ck = cs[k]
+                    slot = 64 + 32 * k
+                    wg3(Dj, ck.cin, gout, 32, ck, g_coff=slot)
+                    kw = dict(m=Dj, m_c0=slot - 32, mslope=LEAKY) if k > 0 else {}
+                    if k == 0 and step == 2:
+                        kw = dict(r2=U, s2=1.0)  # + g_R: the RRDB's own residual
+                    B.append(("conv", ops.conv3x3_desc(gout, 32, ck.bwd, None, ck.cin, gout, x_coff=slot,
+                                                       r1=gout, **kw)))
+            # RRDB input gradient now in V[0:64]; rotate so it becomes the next g_R
+            U, V, W = V, W, U
+        # trunk: g_f0 = chain + g_T, then LeakyReLU'(f0) of conv0
+        B.append(("ew", ops.ew_combine_desc(self.gf0, U, 64, sa=1.0, b=self.gT, sb=1.0, m=f0,
+                                            mslope=self.slope0)))
+        d9h = ops.wgrad9x9_desc(self.dummy_x, self.gf0, _meta_dw(64, 3, 9, dev), None, head=True)
+        B.append(("wg9", d9h, ci[id(self.head)]))
+        self.bwd_launches = B
+        self.head_wg = d9h
+        # workspace for the split-K partial sums
+        nbytes = 0
+        for e in B:
+            if e[0] == "wg3":
+                nbytes = max(nbytes, lib.isr_wgrad3x3_workspace_bytes(ctypes.byref(e[1])))
+            elif e[0] == "wg9":
+                nbytes = max(nbytes, lib.isr_wgrad9x9_workspace_bytes(ctypes.byref(e[1])))
+        if nbytes == 0:
+            raise RuntimeError("train plan: could not size the wgrad workspace: "
+                               + lib.isr_last_error().decode(errors="replace"))
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        # gradient offsets per conv: (w offset, b offset or None)
+        self._conv_goff = []
+        pi = 0
+        for c in self.convs:
+            wo = self._goff[pi]
+            pi += 1
+            bo = None
+            if c.b is not None:
+                bo = self._goff[pi]
+                pi += 1
+            self._conv_goff.append((wo, bo))
+
+    # -------------------------------------------------------------- execution
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x: normalised NCHW fp32 [n, 3, h, w] on the device; returns tanh output."""
+        if tuple(x.shape) != (self.out_shape[0], 3, self.f0.h, self.f0.w) or x.dtype != torch.float32:
+            raise ValueError(f"train plan built for {self.key}, got {tuple(x.shape)} {x.dtype}")
+        x = x.contiguous()
+        self.x = x
+        y = torch.empty(self.out_shape, device=self.device)
+        self.head_desc.x = x.data_ptr()
+        self.tail_desc.y = y.data_ptr()
+        self.head_wg.p = x.data_ptr()
+        st = ops._stream()
+        byref = ctypes.byref
+        for fn, d in self.fwd_launches:
+            rc = fn(byref(d), st)
+            if rc != 0:
+                ops.check(rc, "train forward")
+        self.y = y
+        return y
+
+    def backward(self, gy: torch.Tensor) -> list[torch.Tensor]:
+        """gy: dL/d(output) NCHW fp32.  Returns gradients aligned with params()."""
+        torch.mul(gy, 1.0 - self.y * self.y, out=self.gp)  # tanh' (utils/models.py:607 act=Tanh)
+        grads = torch.empty(self._gsize, device=self.device)
+        gbase = grads.data_ptr()
+        lib, st, byref = self.lib, ops._stream(), ctypes.byref
+        ws, wsn = self.ws.data_ptr(), self.ws.numel()
+        for e in self.bwd_launches:
+            kind, d = e[0], e[1]
+            if kind == "conv":
+                rc = lib.isr_conv3x3_fwd(byref(d), st)
+            elif kind == "wg3" or kind == "wg9":
+                wo, bo = self._conv_goff[e[2]]
+                d.dw = gbase + 4 * wo
+                d.db = gbase + 4 * bo if bo is not None else None
+                rc = (lib.isr_wgrad3x3 if kind == "wg3" else lib.isr_wgrad9x9)(byref(d), ws, wsn, st)
+            elif kind == "head":
+                rc = lib.isr_head9x9_fwd(byref(d), st)
+            else:
+                rc = lib.isr_ew_combine(byref(d), st)
+            if rc != 0:
+                ops.check(rc, f"train backward ({kind})")
+        out = []
+        for p, off in zip(self._params, self._goff):
+            out.append(grads[off:off + p.numel()].view(p.shape))
+        return out
+
+
+def _meta_dw(cout: int, cin: int, k: int, dev) -> torch.Tensor:
+    """Shape-valid placeholder for descriptor construction; the real dw/db
+    pointers are patched per backward call."""
+    return _PLACEHOLDER.setdefault((cout, cin, k, str(dev)), torch.empty(cout, cin, k, k, device=dev))
+
+
+_PLACEHOLDER: dict = {}
+
+
+class _GeneratorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan, *params):
+        ctx.plan = plan
+        return plan.forward(x)
+
+    @staticmethod
+    def backward(ctx, gy):
+        grads = ctx.plan.backward(gy.contiguous().float())
+        return (None, None, *grads)
+
+
+def get_train_plan(gen: nn.Module, x: torch.Tensor) -> GeneratorTrainPlan:
+    n, _, h, w = x.shape
+    key = (n, h, w, str(x.device))
+    plan = gen.__dict__.get("_isr_train_plan")
+    if plan is None or plan.key != key:
+        gen.__dict__["_isr_train_plan"] = None
+        plan = GeneratorTrainPlan(gen, n, h, w, x.device)
+        gen.__dict__["_isr_train_plan"] = plan
+    return plan
+
+
+def train_forward(gen: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """Differentiable generator forward on the HIP path (train mode)."""
+    plan = get_train_plan(gen, x)
+    plan.pack()
+    return _GeneratorFn.apply(x.float().contiguous(), plan, *plan.params())

@@ -71,7 +71,7 @@ typedef struct isr_conv_desc {
     isr_view r1, r2;   /* optional residuals (data == NULL → none), cout channels */
     const void* wpack; /* from isr_pack_conv3x3 */
     const float* bias; /* [cout] fp32 or NULL */
-    float slope, s1, s2;
+    float slope, s1, s2; /* s2 multiplies after r1 even without r2: set 1.0 when unused */
     int32_t shuffle;   /* 1 = plain store, 2 = PixelShuffle(2) store */
     /* Backward-pass extensions (all zero in the forward).  The epilogue order is
      * v = act(acc + bias); v = v*s1 + r1; v = v*s2 + r2; v *= mask; store.
@@ -168,6 +168,18 @@ int isr_wgrad9x9(const isr_wgrad9_desc* d, void* workspace, size_t ws_bytes, isr
 
 size_t isr_wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
 int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
+
+/* Elementwise combine on channel-blocked views (backward glue):
+ *   y = (a*sa + b*sb) * (m > 0 ? 1 : mslope)   over c channels; b, m optional;
+ * y is zero outside the valid h x w region.  Replaces the autograd sum at the
+ * generator trunk (utils/models.py:615, :647: inputs + conv1(residual(inputs)))
+ * and conv0's LeakyReLU backward. */
+typedef struct isr_ew_desc {
+    int32_t n, h, w, ha, wa, c;
+    isr_view y, a, b, m;
+    float sa, sb, mslope;
+} isr_ew_desc;
+int isr_ew_combine(const isr_ew_desc* d, isr_stream_t s);
 
 /* Weight packing (device fp32 OIHW → device bf16 kernel layout).  Replaces the
  * one-off fuse step's weight preparation (utils/models.py:741-751); BN folding

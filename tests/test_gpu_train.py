@@ -1,0 +1,87 @@
+"""Generator training path (train_engine.py) vs autograd through the fp32 oracle.
+
+The oracle graph (oracle/ref_cpu.generator) is pinned to the reference's own
+forward outputs (tests/golden); its gradients are plain autograd of that
+graph.  The HIP path stores activations and gradients in bf16 and accumulates
+in fp32, so per-tensor gradients are compared by relative L2 error (<= 5%)
+and cosine similarity (>= 0.998); the loss itself to 1e-3 relative.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from image_super_resolution_amd import models
+from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_state_dict
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib(built_lib):
+    return built_lib
+
+
+def _oracle_grads(sd, x, hr, blocks, scale, loss_fn):
+    sdc = {k: v.detach().clone().float().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
+    y = R.generator(sdc, x, num_blocks=blocks, scale=scale, enchant=True)
+    loss = loss_fn(y, hr)
+    loss.backward()
+    return loss.item(), {k: v.grad for k, v in sdc.items() if v.grad is not None}
+
+
+@pytest.mark.parametrize("blocks,scale,n,h,w,loss", [(1, 4, 2, 20, 24, "mse"), (2, 2, 2, 36, 40, "l1"),
+                                                     (1, 4, 1, 33, 17, "mse")])
+def test_eresnet_train_step_grads(blocks, scale, n, h, w, loss):
+    torch.manual_seed(0)
+    m = models.EResNet(blocks, 0.2, scale)
+    m.load_state_dict(synth_state_dict(m.state_dict(), 7))
+    lr, hr01 = synth_lr_batch(n, h, w, seed=11, scale=scale)
+    x = normalize(lr)
+    hr = hr01 * 2 - 1
+    loss_fn = F.mse_loss if loss == "mse" else F.l1_loss
+    ref_loss, ref_g = _oracle_grads(m.state_dict(), x, hr, blocks, scale, loss_fn)
+
+    m = m.to(DEV).train()
+    y = m(x.to(DEV))
+    l = loss_fn(y, hr.to(DEV))
+    l.backward()
+    torch.cuda.synchronize()
+    assert abs(l.item() - ref_loss) <= 1e-3 * abs(ref_loss) + 1e-5, (l.item(), ref_loss)
+    worst = []
+    for name, p in m.named_parameters():
+        g = p.grad
+        assert g is not None, name
+        r = ref_g[name].to(DEV)
+        rel = ((g - r).norm() / r.norm().clamp_min(1e-12)).item()
+        cos = F.cosine_similarity(g.flatten(), r.flatten(), dim=0).item()
+        worst.append((rel, cos, name))
+        assert rel <= 5e-2 and cos >= 0.998, f"{name}: rel {rel:.3e} cos {cos:.5f}"
+    worst.sort(reverse=True)
+    print("worst grads:", worst[:3])
+
+
+def test_train_step_updates_and_repacks():
+    """Two optimiser steps: the packed weights follow the parameters (loss changes
+    the way the fp32 reference's does)."""
+    m = models.EResNet(1, 0.2, 2)
+    m.load_state_dict(synth_state_dict(m.state_dict(), 3))
+    lr, hr01 = synth_lr_batch(2, 16, 16, seed=5, scale=2)
+    x, hr = normalize(lr), hr01 * 2 - 1
+    ref = models.EResNet(1, 0.2, 2)
+    ref.load_state_dict(m.state_dict())
+    sd_ref = {k: v.clone().requires_grad_(True) for k, v in ref.state_dict().items()}
+    opt_ref = torch.optim.SGD(list(sd_ref.values()), lr=0.05)
+    m = m.to(DEV).train()
+    opt = torch.optim.SGD(m.parameters(), lr=0.05)
+    for _ in range(2):
+        opt.zero_grad()
+        l = F.mse_loss(m(x.to(DEV)), hr.to(DEV))
+        l.backward()
+        opt.step()
+        opt_ref.zero_grad()
+        lr_ = F.mse_loss(R.generator(sd_ref, x, num_blocks=1, scale=2, enchant=True), hr)
+        lr_.backward()
+        opt_ref.step()
+        assert abs(l.item() - lr_.item()) <= 2e-3 * abs(lr_.item()), (l.item(), lr_.item())
