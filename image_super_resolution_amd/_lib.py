@@ -63,6 +63,17 @@ class IsrEwDesc(ctypes.Structure):
                 ("sa", c_float), ("sb", c_float), ("mslope", c_float)]
 
 
+class IsrConvertDesc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32), ("c", c_int32),
+                ("nchw", c_void_p), ("v", IsrView), ("scale", c_void_p), ("shift", c_void_p),
+                ("m", IsrView), ("mslope", c_float)]
+
+
+class IsrPoolDesc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32), ("hao", c_int32), ("wao", c_int32),
+                ("x", IsrView), ("y", IsrView), ("g", IsrView), ("mslope", c_float)]
+
+
 # Every symbol include/isr.h declares, with its ctypes signature.
 SIGNATURES = {
     "isr_conv3x3_packed_bytes": (c_size_t, [c_int32, c_int32]),
@@ -73,6 +84,10 @@ SIGNATURES = {
     "isr_wgrad9x9_workspace_bytes": (c_size_t, [POINTER(IsrWgrad9Desc)]),
     "isr_wgrad9x9": (c_int32, [POINTER(IsrWgrad9Desc), c_void_p, c_size_t, c_void_p]),
     "isr_ew_combine": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
+    "isr_nchw_to_blocked": (c_int32, [POINTER(IsrConvertDesc), c_void_p]),
+    "isr_blocked_to_nchw": (c_int32, [POINTER(IsrConvertDesc), c_void_p]),
+    "isr_maxpool2_fwd": (c_int32, [POINTER(IsrPoolDesc), c_void_p]),
+    "isr_maxpool2_bwd": (c_int32, [POINTER(IsrPoolDesc), c_void_p]),
     "isr_head9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),
     "isr_pack_head9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "isr_tail9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),

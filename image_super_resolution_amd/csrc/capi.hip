@@ -20,6 +20,9 @@ int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale, int sub2, hipStream_t s);
 int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s);
+int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s);
+int blocked_to_nchw_dispatch(const isr_convert_desc* d, hipStream_t s);
+int maxpool2_dispatch(const isr_pool_desc* d, int backward, hipStream_t s);
 size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
 size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
 int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
@@ -78,7 +81,7 @@ size_t isr_tail9x9_packed_bytes(int32_t cout, int32_t cin) { (void)cout; (void)c
 
 int isr_pack_conv3x3(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
     if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_conv3x3: null pointer");
-    if (cin <= 0 || cin % 32) return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cin %d must be a positive multiple of 32", cin);
+    if (cin <= 0 || cin % 16) return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cin %d must be a positive multiple of 16", cin);
     if (cout <= 0 || cout % 32)
         return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3: cout %d must be a positive multiple of 32", cout);
     return launched(isr::conv3x3_pack(w, packed, cout, cin, (hipStream_t)s), "pack_conv3x3");
@@ -111,7 +114,7 @@ static int conv3x3_validate(const isr_conv_desc* d) {
     if (d->ha % ISR_TILE_H || d->wa % ISR_TILE_W || d->ha < d->h || d->wa < d->w)
         return fail(ISR_ERR_BAD_DESC, "conv3x3: computed region %dx%d must cover %dx%d and be a multiple of %dx%d", d->ha, d->wa,
                     d->h, d->w, ISR_TILE_H, ISR_TILE_W);
-    if (d->cin <= 0 || d->cin % 32) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cin %d must be a multiple of 32", d->cin);
+    if (d->cin <= 0 || d->cin % 16) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cin %d must be a multiple of 16", d->cin);
     if (d->cout <= 0 || d->cout % 32)
         return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cout %d must be a positive multiple of 32", d->cout);
     if (!d->wpack) return fail(ISR_ERR_BAD_DESC, "conv3x3: null weights");
@@ -253,6 +256,51 @@ int isr_ew_combine(const isr_ew_desc* d, isr_stream_t s) {
     if (d->b.data && !view_ok(d->b, d->ha, d->wa, 0, d->c, "ew.b", 1)) return ISR_ERR_BAD_DESC;
     if (d->m.data && !view_ok(d->m, d->ha, d->wa, 0, d->c, "ew.m", 1)) return ISR_ERR_BAD_DESC;
     return launched(isr::ew_combine_dispatch(d, (hipStream_t)s), "ew_combine");
+}
+
+static int convert_validate(const isr_convert_desc* d, const char* who) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "%s: null descriptor", who);
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0) return fail(ISR_ERR_BAD_DESC, "%s: empty problem", who);
+    if (d->ha < d->h || d->wa < d->w) return fail(ISR_ERR_BAD_DESC, "%s: computed region smaller than valid", who);
+    if (!d->nchw) return fail(ISR_ERR_BAD_DESC, "%s: null nchw pointer", who);
+    if (!view_ok(d->v, d->ha, d->wa, 0, (d->c + 15) / 16 * 16, who, 1)) return ISR_ERR_BAD_DESC;
+    if (d->m.data && !view_ok(d->m, d->ha, d->wa, 0, (d->c + 15) / 16 * 16, who, 1)) return ISR_ERR_BAD_DESC;
+    return ISR_OK;
+}
+
+int isr_nchw_to_blocked(const isr_convert_desc* d, isr_stream_t s) {
+    int rc = convert_validate(d, "nchw_to_blocked");
+    if (rc != ISR_OK) return rc;
+    return launched(isr::nchw_to_blocked_dispatch(d, (hipStream_t)s), "nchw_to_blocked");
+}
+
+int isr_blocked_to_nchw(const isr_convert_desc* d, isr_stream_t s) {
+    int rc = convert_validate(d, "blocked_to_nchw");
+    if (rc != ISR_OK) return rc;
+    return launched(isr::blocked_to_nchw_dispatch(d, (hipStream_t)s), "blocked_to_nchw");
+}
+
+static int pool_validate(const isr_pool_desc* d, int bwd) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "maxpool2: null descriptor");
+    if (d->n <= 0 || d->h < 2 || d->w < 2 || d->c <= 0 || d->c % 16)
+        return fail(ISR_ERR_BAD_DESC, "maxpool2: bad problem n=%d h=%d w=%d c=%d", d->n, d->h, d->w, d->c);
+    if (d->hao < d->h / 2 || d->wao < d->w / 2) return fail(ISR_ERR_BAD_DESC, "maxpool2: output region too small");
+    if (!view_ok(d->x, 2 * d->hao, 2 * d->wao, 0, d->c, "maxpool2.x", 1)) return ISR_ERR_BAD_DESC;
+    if (!view_ok(d->y, d->hao, d->wao, 0, d->c, "maxpool2.y", 1)) return ISR_ERR_BAD_DESC;
+    if (bwd && !view_ok(d->g, 2 * d->hao, 2 * d->wao, 0, d->c, "maxpool2.g", 1)) return ISR_ERR_BAD_DESC;
+    return ISR_OK;
+}
+
+int isr_maxpool2_fwd(const isr_pool_desc* d, isr_stream_t s) {
+    int rc = pool_validate(d, 0);
+    if (rc != ISR_OK) return rc;
+    return launched(isr::maxpool2_dispatch(d, 0, (hipStream_t)s), "maxpool2_fwd");
+}
+
+int isr_maxpool2_bwd(const isr_pool_desc* d, isr_stream_t s) {
+    int rc = pool_validate(d, 1);
+    if (rc != ISR_OK) return rc;
+    return launched(isr::maxpool2_dispatch(d, 1, (hipStream_t)s), "maxpool2_bwd");
 }
 
 }  // extern "C"

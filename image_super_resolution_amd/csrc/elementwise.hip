@@ -47,3 +47,158 @@ int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s) {
 }
 
 }  // namespace isr
+
+namespace isr {
+
+// NCHW fp32 → channel-blocked bf16 (channels [0, round16(c)), zero padded), with
+// optional per-channel affine and LeakyReLU' mask; zeros outside the valid region.
+__global__ __launch_bounds__(256) void nchw_to_blocked_kernel(isr_convert_desc d) {
+    const int cp = (d.c + 15) / 16;
+    const size_t total = (size_t)d.n * cp * d.ha * d.wa;
+    const size_t plane = (size_t)d.h * d.w;
+    const float* src = (const float*)d.nchw;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        size_t r = i;
+        const int x = r % d.wa; r /= d.wa;
+        const int y = r % d.ha; r /= d.ha;
+        const int pl = r % cp;
+        const int img = (int)(r / cp);
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = 0.f;
+        const bool valid = y < d.h && x < d.w;
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int c = pl * 16 + k;
+                if (c < d.c) {
+                    float t = src[((size_t)img * d.c + c) * plane + (size_t)y * d.w + x];
+                    if (d.scale) t *= d.scale[c];
+                    if (d.shift) t += d.shift[c];
+                    v[k] = t;
+                }
+            }
+            if (d.m.data) {
+                float m[8];
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    load8_bf16(view_at(d.m, img, y, x, pl * 16 + hf * 8), m);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) v[hf * 8 + k] = m[k] > 0.f ? v[hf * 8 + k] : v[hf * 8 + k] * d.mslope;
+                }
+            }
+        }
+        char* p = view_at(d.v, img, y, x, pl * 16);
+        store8_bf16(p, v);
+        store8_bf16(p + 16, v + 8);
+    }
+}
+
+// channel-blocked bf16 → NCHW fp32 (channels [0, c), valid region only)
+__global__ __launch_bounds__(256) void blocked_to_nchw_kernel(isr_convert_desc d) {
+    const size_t total = (size_t)d.n * d.c * d.h * d.w;
+    const size_t plane = (size_t)d.h * d.w;
+    float* dst = (float*)d.nchw;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % d.w);
+        const int y = (int)((i / d.w) % d.h);
+        const size_t ic = i / plane;
+        const int c = (int)(ic % d.c), img = (int)(ic / d.c);
+        const __bf16 v = *reinterpret_cast<const __bf16*>(view_at(d.v, img, y, x, c));
+        float t = (float)v;
+        if (d.scale) t *= d.scale[c];
+        if (d.shift) t += d.shift[c];
+        dst[i] = t;
+    }
+}
+
+// 2x2 / stride-2 max pool on blocked views (utils/models.py:454-510 via torchvision
+// vgg19.features MaxPool2d(2, 2)); output grid (h/2, w/2), computed region (ha_o, wa_o).
+__global__ __launch_bounds__(256) void maxpool2_fwd_kernel(isr_pool_desc d) {
+    const int cg = d.c / 8;
+    const int ho = d.h / 2, wo = d.w / 2;
+    const size_t total = (size_t)d.n * d.hao * d.wao * cg;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        size_t r = i;
+        const int half = r % 2; r /= 2;
+        const int x = r % d.wao; r /= d.wao;
+        const int y = r % d.hao; r /= d.hao;
+        const int pl = r % (d.c / 16);
+        const int img = (int)(r / (d.c / 16));
+        const int c = pl * 16 + half * 8;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (y < ho && x < wo) {
+            float t[8];
+            load8_bf16(view_at(d.x, img, 2 * y, 2 * x, c), v);
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                load8_bf16(view_at(d.x, img, 2 * y + (q >> 1), 2 * x + (q & 1), c), t);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = t[k] > v[k] ? t[k] : v[k];
+            }
+        }
+        store8_bf16(view_at(d.y, img, y, x, c), v);
+    }
+}
+
+// backward: g_in at the first maximum of each window (PyTorch's scan order, row-major)
+// = g_out, times (x > 0 ? 1 : mslope) — the ReLU' of the layer that produced x.
+__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(isr_pool_desc d) {
+    const int cg = d.c / 8;
+    const int ho = d.h / 2, wo = d.w / 2;
+    const size_t total = (size_t)d.n * d.hao * d.wao * cg;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        size_t r = i;
+        const int half = r % 2; r /= 2;
+        const int x = r % d.wao; r /= d.wao;
+        const int y = r % d.hao; r /= d.hao;
+        const int pl = r % (d.c / 16);
+        const int img = (int)(r / (d.c / 16));
+        const int c = pl * 16 + half * 8;
+        float win[4][8], go[8], best[8];
+        int arg[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) load8_bf16(view_at(d.x, img, 2 * y + (q >> 1), 2 * x + (q & 1), c), win[q]);
+        const bool valid = y < ho && x < wo;
+        if (valid) load8_bf16(view_at(d.y, img, y, x, c), go);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { best[k] = win[0][k]; arg[k] = 0; }
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (win[q][k] > best[k]) { best[k] = win[q][k]; arg[k] = q; }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float o[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float gk = (valid && arg[k] == q) ? go[k] : 0.f;
+                o[k] = win[q][k] > 0.f ? gk : gk * d.mslope;
+            }
+            store8_bf16(view_at(d.g, img, 2 * y + (q >> 1), 2 * x + (q & 1), c), o);
+        }
+    }
+}
+
+static int blocks_for(size_t total) { return (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192); }
+
+int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s) {
+    hipLaunchKernelGGL(nchw_to_blocked_kernel, dim3(blocks_for((size_t)d->n * ((d->c + 15) / 16) * d->ha * d->wa)),
+                       dim3(256), 0, s, *d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int blocked_to_nchw_dispatch(const isr_convert_desc* d, hipStream_t s) {
+    hipLaunchKernelGGL(blocked_to_nchw_kernel, dim3(blocks_for((size_t)d->n * d->c * d->h * d->w)), dim3(256), 0, s, *d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int maxpool2_dispatch(const isr_pool_desc* d, int backward, hipStream_t s) {
+    const size_t total = (size_t)d->n * d->hao * d->wao * (d->c / 8);
+    if (backward) hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, s, *d);
+    else hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, s, *d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace isr

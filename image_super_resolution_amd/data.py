@@ -1,0 +1,107 @@
+"""Training data for the SR generator (utils/datasets.py:274-355 SR_dataset).
+
+The reference decodes, crops, resizes and normalises every sample on CPU
+workers (cv2 + albumentations).  Here the CPU side only decodes and crops
+(uint8, the smallest thing to move); resize to LR, Normalize and the HR
+transform (PIL_to_tanh, utils/datasets.py:96-106, or Normalize for SRGAN
+mode, :336-339) run batched on the GPU (`GPUTransform`).  `SyntheticSR`
+generates smooth random HR crops directly on the GPU (no dataset is
+available offline; SURVEY.md §8d's synthetic recipe).
+"""
+from __future__ import annotations
+
+import json
+import random
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch.utils.data import Dataset
+
+IMG_FORMATS = (".bmp", ".jpg", ".jpeg", ".png", ".tif", ".tiff", ".webp")
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def ground_up(x: int, factor: int) -> int:
+    """utils/general.py ground_up: round x up to a multiple of factor."""
+    return (x + factor - 1) // factor * factor
+
+
+def list_images(src) -> list[str]:
+    """A JSON list of paths (train.py:191 train_images.json) or a directory."""
+    src = Path(src)
+    if src.suffix == ".json":
+        with open(src) as f:
+            return [str(p) for p in json.load(f)]
+    return sorted(str(p) for p in src.rglob("*") if p.suffix.lower() in IMG_FORMATS)
+
+
+class SRCropDataset(Dataset):
+    """Random `target_size` RGB crops as uint8 CHW (SR_dataset's RandomCrop,
+    utils/datasets.py:288, 344-347); images smaller than the crop are padded."""
+
+    def __init__(self, src, target_size: int, scale: int, prefix: str = ""):
+        self.samples = list_images(src)
+        if not self.samples:
+            raise FileNotFoundError(f"no images under {src}")
+        self.target_size = ground_up(target_size, scale)
+        self.scale = scale
+        print(f"{prefix}{len(self.samples)} images with target shape {self.target_size} with scale factor {scale}.")
+
+    def __len__(self):
+        return len(self.samples)
+
+    def __getitem__(self, i):
+        from PIL import Image
+        with Image.open(self.samples[i]) as im:
+            a = np.asarray(im.convert("RGB"))
+        t = self.target_size
+        h, w = a.shape[:2]
+        if h < t or w < t:
+            a = np.pad(a, ((0, max(0, t - h)), (0, max(0, t - w)), (0, 0)), mode="reflect")
+            h, w = a.shape[:2]
+        y, x = random.randint(0, h - t), random.randint(0, w - t)
+        return torch.from_numpy(np.ascontiguousarray(a[y:y + t, x:x + t])).permute(2, 0, 1).contiguous()
+
+
+class GPUTransform:
+    """Batched (hr, lr) from uint8 HR crops on the device:
+    lr = Normalize(Resize(crop, T/scale)) (albumentations Resize = cv2 INTER_LINEAR,
+    utils/datasets.py:302-303); hr = 2*crop/255 - 1 (PIL_to_tanh) or
+    Normalize(crop) when hr_norm (set_transform_hr, SRGAN mode)."""
+
+    def __init__(self, scale: int, hr_norm: bool = False, mean=IMAGENET_MEAN, std=IMAGENET_STD, device="cuda"):
+        self.scale, self.hr_norm = scale, hr_norm
+        self.mean = torch.tensor(mean, device=device).view(1, 3, 1, 1)
+        self.std = torch.tensor(std, device=device).view(1, 3, 1, 1)
+        self.device = device
+
+    def __call__(self, crops_u8: torch.Tensor):
+        x = crops_u8.to(self.device, non_blocking=True).float().div_(255.0)
+        t = x.shape[-1]
+        lr = F.interpolate(x, size=(t // self.scale, t // self.scale), mode="bilinear", align_corners=False,
+                           antialias=False)
+        lr = (lr - self.mean) / self.std
+        hr = (x - self.mean) / self.std if self.hr_norm else x * 2.0 - 1.0
+        return hr.contiguous(), lr.contiguous()
+
+
+class SyntheticSR:
+    """Endless synthetic uint8 HR crops on the GPU: bicubic-upsampled 32x32
+    uniform noise (a smooth 'natural-ish' image), seed per batch and rank."""
+
+    def __init__(self, batch: int, target_size: int, seed: int = 0, device="cuda"):
+        self.batch, self.t, self.seed, self.device = batch, target_size, seed, device
+        self.i = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> torch.Tensor:
+        g = torch.Generator(device=self.device).manual_seed(self.seed * 1_000_003 + self.i)
+        self.i += 1
+        base = torch.rand(self.batch, 3, 32, 32, generator=g, device=self.device)
+        hr = F.interpolate(base, size=(self.t, self.t), mode="bicubic", align_corners=False).clamp_(0, 1)
+        return (hr * 255).round_().to(torch.uint8)

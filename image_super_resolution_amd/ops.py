@@ -12,7 +12,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._lib import IsrConvDesc, IsrEwDesc, IsrHeadDesc, IsrTailDesc, IsrView, IsrWgrad9Desc, IsrWgradDesc, TILE_H, TILE_W, check
+from ._lib import IsrConvDesc, IsrConvertDesc, IsrEwDesc, IsrHeadDesc, IsrPoolDesc, IsrTailDesc, IsrView, IsrWgrad9Desc, IsrWgradDesc, TILE_H, TILE_W, check
 
 
 def round_up(v: int, m: int) -> int:
@@ -372,3 +372,51 @@ def ew_combine_desc(y: ActBuffer, a: ActBuffer, c: int, *, sa: float = 1.0, b: A
 
 def ew_combine(y: ActBuffer, a: ActBuffer, c: int, **kw) -> None:
     check(_lib.load().isr_ew_combine(ctypes.byref(ew_combine_desc(y, a, c, **kw)), _stream()), "isr_ew_combine")
+
+
+def convert_desc(nchw: torch.Tensor, v: ActBuffer, *, v_coff: int = 0, scale: torch.Tensor | None = None,
+                 shift: torch.Tensor | None = None, m: ActBuffer | None = None, mslope: float = 1.0,
+                 m_coff: int = 0) -> IsrConvertDesc:
+    _require_gpu(nchw, "convert")
+    if nchw.dtype != torch.float32 or not nchw.is_contiguous() or nchw.dim() != 4:
+        raise ValueError("convert: nchw must be contiguous fp32 [n, c, h, w]")
+    n, c, h, w = nchw.shape
+    if (n, h, w) != (v.n, v.h, v.w):
+        raise ValueError(f"convert: grid mismatch {tuple(nchw.shape)} vs buffer {(v.n, v.h, v.w)}")
+    d = IsrConvertDesc()
+    d.n, d.h, d.w, d.ha, d.wa, d.c = n, h, w, v.ha, v.wa, c
+    d.nchw = nchw.data_ptr()
+    d.v = v.view(v_coff)
+    d.scale = scale.data_ptr() if scale is not None else None
+    d.shift = shift.data_ptr() if shift is not None else None
+    d.m = m.view(m_coff) if m is not None else _NULL_VIEW
+    d.mslope = mslope
+    return d
+
+
+def nchw_to_blocked(nchw: torch.Tensor, v: ActBuffer, **kw) -> None:
+    check(_lib.load().isr_nchw_to_blocked(ctypes.byref(convert_desc(nchw, v, **kw)), _stream()), "isr_nchw_to_blocked")
+
+
+def blocked_to_nchw(v: ActBuffer, out: torch.Tensor, **kw) -> torch.Tensor:
+    check(_lib.load().isr_blocked_to_nchw(ctypes.byref(convert_desc(out, v, **kw)), _stream()), "isr_blocked_to_nchw")
+    return out
+
+
+def pool_desc(x: ActBuffer, y: ActBuffer, c: int, g: ActBuffer | None = None, mslope: float = 0.0) -> IsrPoolDesc:
+    if (y.h, y.w) != (x.h // 2, x.w // 2) or y.ha * 2 > x.ha or y.wa * 2 > x.wa:
+        raise ValueError("maxpool2: output grid must be (h/2, w/2) with 2*ha_out within the input buffer")
+    d = IsrPoolDesc()
+    d.n, d.h, d.w, d.c, d.hao, d.wao = x.n, x.h, x.w, c, y.ha, y.wa
+    d.x, d.y = x.view(0), y.view(0)
+    d.g = g.view(0) if g is not None else _NULL_VIEW
+    d.mslope = mslope
+    return d
+
+
+def maxpool2_fwd(x: ActBuffer, y: ActBuffer, c: int) -> None:
+    check(_lib.load().isr_maxpool2_fwd(ctypes.byref(pool_desc(x, y, c)), _stream()), "isr_maxpool2_fwd")
+
+
+def maxpool2_bwd(x: ActBuffer, gy: ActBuffer, gx: ActBuffer, c: int, mslope: float = 0.0) -> None:
+    check(_lib.load().isr_maxpool2_bwd(ctypes.byref(pool_desc(x, gy, c, gx, mslope)), _stream()), "isr_maxpool2_bwd")

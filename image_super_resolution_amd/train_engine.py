@@ -299,6 +299,13 @@ class GeneratorTrainPlan:
                 rc = lib.isr_ew_combine(byref(d), st)
             if rc != 0:
                 ops.check(rc, f"train backward ({kind})")
+        group = self.gen.__dict__.get("_isr_grad_group")
+        if group is not None:
+            # data-parallel: one RCCL all-reduce of the whole flat gradient buffer
+            # (47.5 MB for the 16-block generator) instead of DDP's per-bucket hooks
+            import torch.distributed as dist
+            dist.all_reduce(grads, group=group if group is not True else None)
+            grads.div_(dist.get_world_size(group if group is not True else None))
         out = []
         for p, off in zip(self._params, self._goff):
             out.append(grads[off:off + p.numel()].view(p.shape))
@@ -342,3 +349,28 @@ def train_forward(gen: nn.Module, x: torch.Tensor) -> torch.Tensor:
     plan = get_train_plan(gen, x)
     plan.pack()
     return _GeneratorFn.apply(x.float().contiguous(), plan, *plan.params())
+
+
+def enable_grad_allreduce(gen: nn.Module, group=True) -> None:
+    """Average the generator's gradients over the process group inside the HIP
+    backward (data parallel; `group=True` = the default group, None disables)."""
+    from .models import SRGAN
+    if isinstance(gen, SRGAN):
+        gen = gen.res_net
+    gen.__dict__["_isr_grad_group"] = group
+
+
+def allreduce_grads(params, group=None) -> None:
+    """Mean of .grad over the group for modules trained outside the HIP plan
+    (the discriminator): one flat all-reduce."""
+    import torch.distributed as dist
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, group=group)
+    flat.div_(dist.get_world_size(group))
+    off = 0
+    for g in grads:
+        g.copy_(flat[off:off + g.numel()].view_as(g))
+        off += g.numel()

@@ -1,0 +1,142 @@
+"""Training loops of train.py (train.py:41-67 `train`, :70-129 `train_srgan`).
+
+Same structure and optimiser semantics as the reference — Adam, LinearLR per
+iteration, clip_grad_norm_(10), ModelEMA after every generator step — with
+the generator forward/backward on the HIP training path (train_engine.py),
+the VGG19 perceptual loss on HIP (vgg.py), and data arriving as uint8 crops
+transformed on the GPU (data.py).
+
+Differences, all deliberate:
+* bf16 storage with fp32 accumulation and fp32 master weights replaces fp16
+  autocast, so the GradScaler is disabled (bf16 has fp32's exponent range);
+  the GradScaler objects are kept for checkpoint compatibility.
+* loss.item() host syncs happen once per `log_every` iterations instead of
+  every iteration (train.py:64-65, :101-112).
+* multi-GPU (one process per GPU): the generator's gradients are averaged by
+  one RCCL all-reduce of its flat gradient buffer inside the HIP backward
+  (train_engine.enable_grad_allreduce); the discriminator's by one flat
+  all-reduce after its backward (allreduce_grads).  Same math as DDP.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+from torch.nn.utils import clip_grad_norm_
+
+from .models import ModelEMA
+from .train_engine import allreduce_grads
+
+
+def _scalar(writer, tag, value, step):
+    if writer is not None:
+        writer.add_scalar(tag, value, step)
+
+
+def _unwrap(m):
+    return m.module if hasattr(m, "module") else m
+
+
+def train(model, ema: ModelEMA, batches, transform, compute_loss, optimizer, gradscaler, schedule, epoch: int,
+          tensorBoard=None, steps: int | None = None, log_every: int = 50):
+    """train.py:41-67: one epoch of pixel-loss (MSE / L1Loss) generator training."""
+    model.train()
+    losses = []
+    total = steps if steps is not None else len(batches)
+    it = iter(batches)
+    pending = []
+    for idx in range(total):
+        hr, lr = transform(next(it))
+        optimizer.zero_grad(set_to_none=True)
+        preds = model(lr)
+        loss = compute_loss(preds, hr)
+        gradscaler.scale(loss).backward()
+        gradscaler.unscale_(optimizer)
+        clip_grad_norm_(model.parameters(), 10)
+        gradscaler.step(optimizer)
+        gradscaler.update()
+        schedule.step()
+        ema.update(_unwrap(model))
+        pending.append(loss.detach())
+        if len(pending) == log_every or idx == total - 1:
+            vals = torch.stack(pending).cpu().tolist()
+            for k, v in enumerate(vals):
+                _scalar(tensorBoard, "loss", v, epoch * total + idx - len(vals) + k + 2)
+            losses += vals
+            pending = []
+    return losses
+
+
+def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_loss, optimizer_g, optimizer_d,
+                gradscaler, schedules, epoch: int, tensorBoard=None, mean=None, std=None,
+                steps: int | None = None, log_every: int = 50, dist_group=None):
+    """train.py:70-129: one epoch of SRGAN training (VGG perceptual + adversarial)."""
+    gen_net.train()
+    dis_net.train()
+    loss_g = []
+    gradscaler_gen, gradscaler_dis = gradscaler
+    schedule_g, schedule_d = schedules
+    device = next(_unwrap(gen_net).parameters()).device
+    mean = torch.tensor(mean, device=device).view(1, 3, 1, 1)
+    std = torch.tensor(std, device=device).view(1, 3, 1, 1)
+    total = steps if steps is not None else len(batches)
+    it = iter(batches)
+    pending = []
+    for idx in range(total):
+        hr_images, lr_images = transform(next(it))
+        sr_images = gen_net(lr_images)
+        sr_images = (sr_images + 1.0) / 2.0
+        sr_images = (sr_images - mean) / std
+        # the discriminator's gradients from the generator loss are discarded
+        # (optimizer_d.zero_grad below), exactly as in the reference
+        sr_discriminated = dis_net(sr_images)
+        perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(sr_images, hr_images,
+                                                                                         sr_discriminated)
+        optimizer_g.zero_grad(set_to_none=True)
+        gradscaler_gen.scale(perceptual_loss).backward()
+        gradscaler_gen.unscale_(optimizer_g)
+        clip_grad_norm_(gen_net.parameters(), 10)
+        gradscaler_gen.step(optimizer_g)
+        gradscaler_gen.update()
+        schedule_g.step()
+        ema.update(_unwrap(gen_net))
+
+        sr_discriminated = dis_net(sr_images.detach())
+        hr_discriminated = dis_net(hr_images)
+        adversarial_loss = compute_loss.calc_advLoss(sr_discriminated, hr_discriminated)
+        optimizer_d.zero_grad(set_to_none=True)
+        gradscaler_dis.scale(adversarial_loss).backward()
+        if dist_group is not None:
+            allreduce_grads(dis_net.parameters(), None if dist_group is True else dist_group)
+        gradscaler_dis.unscale_(optimizer_d)
+        clip_grad_norm_(dis_net.parameters(), 10)
+        gradscaler_dis.step(optimizer_d)
+        gradscaler_dis.update()
+        schedule_d.step()
+        pending.append(torch.stack([content_loss.detach(), adversarial_loss_.detach(), adversarial_loss.detach()]))
+        if len(pending) == log_every or idx == total - 1:
+            vals = torch.stack(pending).cpu().tolist()
+            for k, (c, a, d) in enumerate(vals):
+                step = epoch * total + idx - len(vals) + k + 2
+                _scalar(tensorBoard, "loss/content", c, step)
+                _scalar(tensorBoard, "loss/adv", a, step)
+                _scalar(tensorBoard, "loss/dis", d, step)
+                loss_g.append(c)
+            pending = []
+    return loss_g
+
+
+class StepTimer:
+    """Wall-clock per step with a device sync at the ends (for logs / bench)."""
+
+    def __init__(self):
+        self.t0 = None
+
+    def __enter__(self):
+        torch.cuda.synchronize()
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *a):
+        torch.cuda.synchronize()
+        self.dt = time.perf_counter() - self.t0

@@ -64,7 +64,7 @@ typedef struct isr_view {
 typedef struct isr_conv_desc {
     int32_t n, h, w;   /* batch; valid conv height/width (input == output size) */
     int32_t ha, wa;    /* computed (tile-aligned) extent; ha % 32 == 0, wa % 32 == 0 */
-    int32_t cin, cout; /* cin % 32 == 0; cout % 32 == 0 (cout % 64 != 0 runs 32-cout tiles) */
+    int32_t cin, cout; /* cin % 16 == 0; cout % 32 == 0 (cout % 64 != 0 runs 32-cout tiles) */
     isr_view x;        /* input (cin channels from x.coff) */
     isr_view y;        /* output; for shuffle == 2 its grid is (2h, 2w), cout/4 channels */
     isr_view y2;       /* optional duplicate output (y2.data == NULL → none) */
@@ -180,6 +180,37 @@ typedef struct isr_ew_desc {
     float sa, sb, mslope;
 } isr_ew_desc;
 int isr_ew_combine(const isr_ew_desc* d, isr_stream_t s);
+
+/* Layout conversion between NCHW fp32 tensors and channel-blocked views
+ * (network / loss boundaries: the VGG19 input, utils/loss.py:16-24, and the
+ * gradient it receives).  to_blocked writes channels [0, round16(c)) of v (zeros
+ * past c and outside the valid region), v = x*scale[c] + shift[c] (NULL → 1 / 0),
+ * then the optional LeakyReLU' mask m (ReLU' with mslope 0); to_nchw reads
+ * channels [0, c) of v into nchw, applying scale/shift. */
+typedef struct isr_convert_desc {
+    int32_t n, h, w, ha, wa, c;
+    void* nchw;
+    isr_view v;
+    const float* scale;
+    const float* shift;
+    isr_view m;
+    float mslope;
+} isr_convert_desc;
+int isr_nchw_to_blocked(const isr_convert_desc* d, isr_stream_t s);
+int isr_blocked_to_nchw(const isr_convert_desc* d, isr_stream_t s);
+
+/* 2x2 stride-2 max pool (torchvision vgg19.features MaxPool2d, used by
+ * TruncatedVGG19 utils/models.py:454-510).  Input grid h x w (even), output
+ * (h/2) x (w/2) with computed region hao x wao (multiples of 32).
+ * fwd: y = maxpool(x).  bwd: g (input grid) = y (output gradient) routed to the
+ * first maximum of each window, times (x > 0 ? 1 : mslope). */
+typedef struct isr_pool_desc {
+    int32_t n, h, w, c, hao, wao;
+    isr_view x, y, g;
+    float mslope;
+} isr_pool_desc;
+int isr_maxpool2_fwd(const isr_pool_desc* d, isr_stream_t s);
+int isr_maxpool2_bwd(const isr_pool_desc* d, isr_stream_t s);
 
 /* Weight packing (device fp32 OIHW → device bf16 kernel layout).  Replaces the
  * one-off fuse step's weight preparation (utils/models.py:741-751); BN folding

@@ -72,9 +72,9 @@ def test_validation_rejects_without_touching_gpu(built_lib):
     assert lib.isr_conv3x3_fwd(None, None) == -1
     assert b"null descriptor" in lib.isr_last_error()
     d = _lib.IsrConvDesc()
-    d.n, d.h, d.w, d.ha, d.wa, d.cin, d.cout = 1, 16, 32, 32, 32, 48, 64
+    d.n, d.h, d.w, d.ha, d.wa, d.cin, d.cout = 1, 16, 32, 32, 32, 40, 64
     assert lib.isr_conv3x3_fwd(ctypes.byref(d), None) == -2
-    assert b"multiple of 32" in lib.isr_last_error()
+    assert b"multiple of 16" in lib.isr_last_error()
     d.cin = 64
     d.ha = 16  # not tile aligned (ISR_TILE_H = 32)
     assert lib.isr_conv3x3_fwd(ctypes.byref(d), None) == -1

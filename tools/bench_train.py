@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Training-step throughput: SRGAN-mode step of the 4x
+EResNet generator with the VGG19 conv5_4 (pre-activation, L1) perceptual loss
+and the adversarial term, batch 16 of 128² LR → 512² HR per GPU, Adam + EMA.
+
+python tools/bench_train.py [--steps 5] [--warmup 2] [--mode srgan|pixel]
+Launch with torch.distributed.run for N GPUs (one process per GPU, RCCL).
+Prints one JSON line on rank 0 (HR megapixels/s and samples/s, whole job).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import warnings
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from image_super_resolution_amd import data, loss as L, models, trainer  # noqa: E402
+from image_super_resolution_amd.train_engine import enable_grad_allreduce  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--hr", type=int, default=512)
+    ap.add_argument("--blocks", type=int, default=16)
+    ap.add_argument("--mode", default="srgan", choices=["srgan", "pixel"])
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(dev)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        group = True
+    torch.manual_seed(0)
+    mean, std = list(data.IMAGENET_MEAN), list(data.IMAGENET_STD)
+    batches = data.SyntheticSR(args.batch, args.hr, seed=rank, device=dev)
+    total = args.steps + args.warmup
+    if args.mode == "srgan":
+        gen = models.SRGAN(args.blocks, 0.2, True, 4).to(dev)
+        dis = models.Discriminator(3, 64, 8, 1024).to(dev)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            gl = L.gen_loss(device=dev, beforeAct=True)
+        og = torch.optim.Adam(gen.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        od = torch.optim.Adam(dis.parameters(), lr=1e-4, betas=(0.9, 0.999))
+        sg = torch.optim.lr_scheduler.LinearLR(og, 1, 0.01, total_iters=total)
+        sd = torch.optim.lr_scheduler.LinearLR(od, 1, 0.01, total_iters=total)
+        ema = models.ModelEMA(gen, tau=total)
+        ema.ema.to(dev)
+        if group:
+            enable_grad_allreduce(gen, group)
+        sc = (torch.amp.GradScaler("cuda", enabled=False), torch.amp.GradScaler("cuda", enabled=False))
+        tf = data.GPUTransform(4, hr_norm=True, mean=mean, std=std, device=dev)
+
+        def run(n):
+            trainer.train_srgan(gen, ema, dis, batches, tf, gl, og, od, sc, (sg, sd), 0, None, mean=mean, std=std,
+                                steps=n, log_every=10 ** 9, dist_group=group)
+    else:
+        gen = models.EResNet(args.blocks, 0.2, 4).to(dev)
+        og = torch.optim.Adam(gen.parameters(), lr=1e-4)
+        sg = torch.optim.lr_scheduler.LinearLR(og, 1, 0.01, total_iters=total)
+        ema = models.ModelEMA(gen, tau=total)
+        ema.ema.to(dev)
+        if group:
+            enable_grad_allreduce(gen, group)
+        tf = data.GPUTransform(4, hr_norm=False, mean=mean, std=std, device=dev)
+        l1 = L.L1Loss().to(dev)
+
+        def run(n):
+            trainer.train(gen, ema, batches, tf, l1, og, torch.amp.GradScaler("cuda", enabled=False), sg, 0, None,
+                          steps=n, log_every=10 ** 9)
+    run(args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = torch.tensor(time.perf_counter() - t0, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
+    dt = dt.item()
+    samples = args.steps * args.batch * world
+    if rank == 0:
+        print(json.dumps({"metric": f"{args.mode} train step throughput (4x EResNet, VGG19 5_4 L1 + adv)",
+                          "value": round(samples * args.hr * args.hr / 1e6 / dt, 2), "unit": "HR MPix/s",
+                          "samples_per_s": round(samples / dt, 2), "ms_per_step": round(dt * 1e3 / args.steps, 2),
+                          "n_gpus": world, "global_batch": args.batch * world, "steps": args.steps,
+                          "mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
