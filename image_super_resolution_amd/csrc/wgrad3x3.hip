@@ -19,7 +19,7 @@
 // fragment (X shifted by (dy, dx)) is read per tap.  Pixel tiles are TY rows x
 // 32 columns; each block walks a contiguous range of them (split-K over
 // n*h*w), double-buffered through LDS.  Per-block partial sums go to a
-// workspace [split][tap][co][ci] (+ [split][co] for the bias); a second kernel
+// workspace [split][tap][co][ci | + co bias]; a second kernel
 // reduces over splits, applies `scale`, and writes dW in the reference OIHW
 // layout (and un-permutes the PixelShuffle channel order for g_sub2).
 #include "isr_common.h"
@@ -62,7 +62,7 @@ struct WG {
 
 struct WgradArgs {
     isr_wgrad_desc d;
-    float* ws;  // [splits][9][cout][cin] then [splits][cout]
+    float* ws;  // [splits][9*cout*cin (tap, co, ci) + cout (bias)]
     int splits, tiles;
 };
 
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
 
     // ---- partial sums: ws[split][tap][co][ci], D[co = (g&3)+8(g>>2)+4h][ci = l31]
     const int l31 = lane & 31;
-    float* wsp = a.ws + (size_t)split * 9 * d.cout * d.cin;
+    float* wsp = a.ws + (size_t)split * (9 * d.cout * d.cin + d.cout);
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
         float* wt = wsp + (size_t)(wave * 3 + dx) * d.cout * d.cin;
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
                 }
     }
     if (d.db && cit == 0 && wave == 1) {
-        float* bp = a.ws + (size_t)a.splits * 9 * d.cout * d.cin + (size_t)split * d.cout;
+        float* bp = wsp + (size_t)9 * d.cout * d.cin;
 #pragma unroll
         for (int f = 0; f < NCO; ++f) {
             const float v = bsum[f] + __shfl_xor(bsum[f], 32);
@@ -222,26 +222,42 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
 }
 
 // dW[co][ci][tap] (reference OIHW) = scale * sum_s ws[s][tap][co'][ci];  co' = kernel channel order.
-__global__ void wgrad_reduce_kernel(WgradArgs a) {
+// Workspace rows are [splits][9*cout*cin + cout] (the bias partials follow each
+// split's dW partials).  Block = 4 split-slices x 64 float4 columns: every
+// thread streams S/4 rows of one 16-byte column (independent loads in flight),
+// the 4 slices are summed through LDS.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
+    __shared__ f32x4 red[4][64];
     const isr_wgrad_desc& d = a.d;
     const size_t per = (size_t)9 * d.cout * d.cin;
+    const size_t row = per + d.cout;
+    const int nv = (int)(row / 4);
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int slice = threadIdx.x >> 6;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (col < nv) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.ws) + col;
+#pragma unroll 4
+        for (int sp = slice; sp < a.splits; sp += 4) acc += src[(size_t)sp * (row / 4)];
+    }
+    red[slice][threadIdx.x & 63] = acc;
+    __syncthreads();
+    if (slice != 0 || col >= nv) return;
+    acc = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     const int cs4 = d.cout >> 2;
-    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < per + d.cout;
-         idx += (size_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const size_t idx = (size_t)col * 4 + e;
         if (idx < per) {
             const int ci = (int)(idx % d.cin);
             const int cok = (int)((idx / d.cin) % d.cout);
             const int tap = (int)(idx / ((size_t)d.cin * d.cout));
-            float s = 0.f;
-            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[sp * per + idx];
             const int co = d.g_sub2 ? (cok % cs4) * 4 + cok / cs4 : cok;
-            d.dw[((size_t)co * d.cin + ci) * 9 + tap] = s * d.scale;
+            d.dw[((size_t)co * d.cin + ci) * 9 + tap] = acc[e] * d.scale;
         } else if (d.db) {
             const int cok = (int)(idx - per);
-            float s = 0.f;
-            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[(size_t)a.splits * per + (size_t)sp * d.cout + cok];
             const int co = d.g_sub2 ? (cok % cs4) * 4 + cok / cs4 : cok;
-            d.db[co] = s * d.scale;
+            d.db[co] = acc[e] * d.scale;
         }
     }
 }
@@ -279,7 +295,8 @@ static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipS
     const int blocks = a.splits * (d->cout / C::CO_T) * (d->cin / C::CI_T);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, a);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(512), dim3(256), 0, s, a);
+    const size_t nv = ((size_t)9 * d->cout * d->cin + d->cout) / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nv + 63) / 64)), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

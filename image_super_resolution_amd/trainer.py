@@ -10,6 +10,8 @@ Differences, all deliberate:
 * bf16 storage with fp32 accumulation and fp32 master weights replaces fp16
   autocast, so the GradScaler is disabled (bf16 has fp32's exponent range);
   the GradScaler objects are kept for checkpoint compatibility.
+* the discriminator (stock PyTorch-ROCm ops) runs under bf16
+  autocast where the reference uses fp16 autocast (train.py:91, :114).
 * loss.item() host syncs happen once per `log_every` iterations instead of
   every iteration (train.py:64-65, :101-112).
 * multi-GPU (one process per GPU): the generator's gradients are averaged by
@@ -89,7 +91,8 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
         sr_images = (sr_images - mean) / std
         # the discriminator's gradients from the generator loss are discarded
         # (optimizer_d.zero_grad below), exactly as in the reference
-        sr_discriminated = dis_net(sr_images)
+        with torch.autocast("cuda", dtype=torch.bfloat16):  # the reference runs D under fp16 autocast
+            sr_discriminated = dis_net(sr_images)
         perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(sr_images, hr_images,
                                                                                          sr_discriminated)
         optimizer_g.zero_grad(set_to_none=True)
@@ -101,8 +104,9 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
         schedule_g.step()
         ema.update(_unwrap(gen_net))
 
-        sr_discriminated = dis_net(sr_images.detach())
-        hr_discriminated = dis_net(hr_images)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            sr_discriminated = dis_net(sr_images.detach())
+            hr_discriminated = dis_net(hr_images)
         adversarial_loss = compute_loss.calc_advLoss(sr_discriminated, hr_discriminated)
         optimizer_d.zero_grad(set_to_none=True)
         gradscaler_dis.scale(adversarial_loss).backward()
