@@ -4,6 +4,7 @@
 #   profiles/<R>_pmc_summary.json         per-kernel PMC summary (tools/pmc_summary.py)
 #   profiles/<R>_pmc_traffic.json         HBM bytes per launch of the dominant kernel (read by bench.py)
 #   profiles/<R>_bench.json               the bench line after the traffic file exists
+#   profiles/<R>_train_kernel_stats.csv   rocprofv3 --kernel-trace --stats of tools/bench_train.py (cfg3 step)
 # usage: tools/make_profiles.sh r01
 set -eu
 R=${1:-r01}
@@ -19,7 +20,7 @@ python3 - "$R" "$P" <<'EOF'
 import json, sys
 R, P = sys.argv[1], sys.argv[2]
 rows = json.load(open(f"{P}/{R}_pmc_summary.json"))
-dom = [r for r in rows if "192>" in r["kernel"]]
+dom = [r for r in rows if "192, 0, 0>" in r["kernel"] or "192>" in r["kernel"]]  # RDB final conv (V_F0)
 if dom:
     r = dom[0]
     out = {"kernel": r["kernel"], "grid": r["grid"], "dispatches": r["dispatches"],
@@ -34,3 +35,6 @@ EOF
 cp $P/${R}_pmc_traffic.json profiles/ 2>/dev/null || true
 timeout -k 10 600 python3 bench.py --round $R > $P/${R}_bench.json 2> gpurun_out/bench_final_$R.err
 cat $P/${R}_bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_train_$R -o train -- \
+  python3 tools/bench_train.py --steps 3 --warmup 2 > $P/${R}_train_bench.json 2> gpurun_out/prof_train_$R.err
+cp gpurun_out/prof_train_$R/train_kernel_stats.csv $P/${R}_train_kernel_stats.csv
