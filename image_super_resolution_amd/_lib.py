@@ -74,6 +74,15 @@ class IsrPoolDesc(ctypes.Structure):
                 ("x", IsrView), ("y", IsrView), ("g", IsrView), ("mslope", c_float)]
 
 
+class IsrBnDesc(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32), ("c", c_int32),
+                ("z", IsrView), ("y", IsrView), ("r1", IsrView), ("r2", IsrView), ("dz", IsrView),
+                ("s1", c_float), ("s2", c_float), ("slope", c_float),
+                ("gamma", c_void_p), ("beta", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
+                ("momentum", c_float), ("eps", c_float), ("acc", c_void_p), ("save", c_void_p),
+                ("dgamma", c_void_p), ("dbeta", c_void_p), ("gscale", c_float)]
+
+
 # Every symbol include/isr.h declares, with its ctypes signature.
 SIGNATURES = {
     "isr_conv3x3_packed_bytes": (c_size_t, [c_int32, c_int32]),
@@ -84,6 +93,11 @@ SIGNATURES = {
     "isr_wgrad9x9_workspace_bytes": (c_size_t, [POINTER(IsrWgrad9Desc)]),
     "isr_wgrad9x9": (c_int32, [POINTER(IsrWgrad9Desc), c_void_p, c_size_t, c_void_p]),
     "isr_ew_combine": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
+    "isr_bn_stats": (c_int32, [POINTER(IsrBnDesc), c_void_p]),
+    "isr_bn_finalize": (c_int32, [POINTER(IsrBnDesc), c_void_p]),
+    "isr_bn_apply": (c_int32, [POINTER(IsrBnDesc), c_void_p]),
+    "isr_bn_bwd_reduce": (c_int32, [POINTER(IsrBnDesc), c_void_p]),
+    "isr_bn_bwd_apply": (c_int32, [POINTER(IsrBnDesc), c_void_p]),
     "isr_nchw_to_blocked": (c_int32, [POINTER(IsrConvertDesc), c_void_p]),
     "isr_blocked_to_nchw": (c_int32, [POINTER(IsrConvertDesc), c_void_p]),
     "isr_maxpool2_fwd": (c_int32, [POINTER(IsrPoolDesc), c_void_p]),

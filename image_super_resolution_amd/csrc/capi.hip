@@ -20,6 +20,7 @@ int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale, int sub2, hipStream_t s);
 int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s);
+int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s);
 int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s);
 int blocked_to_nchw_dispatch(const isr_convert_desc* d, hipStream_t s);
 int maxpool2_dispatch(const isr_pool_desc* d, int backward, hipStream_t s);
@@ -302,5 +303,34 @@ int isr_maxpool2_bwd(const isr_pool_desc* d, isr_stream_t s) {
     if (rc != ISR_OK) return rc;
     return launched(isr::maxpool2_dispatch(d, 1, (hipStream_t)s), "maxpool2_bwd");
 }
+
+static int bn_validate(const isr_bn_desc* d, int op) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "bn: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0 || d->c % 16)
+        return fail(ISR_ERR_BAD_DESC, "bn: bad problem n=%d h=%d w=%d c=%d", d->n, d->h, d->w, d->c);
+    if (d->ha < d->h || d->wa < d->w) return fail(ISR_ERR_BAD_DESC, "bn: computed region smaller than valid");
+    if (!d->acc || !d->save) return fail(ISR_ERR_BAD_DESC, "bn: null acc / save");
+    if (op != 1 && !view_ok(d->z, d->ha, d->wa, 0, d->c, "bn.z", 1)) return ISR_ERR_BAD_DESC;
+    if ((op == 2 || op >= 3) && !view_ok(d->y, d->ha, d->wa, 0, d->c, "bn.y", 1)) return ISR_ERR_BAD_DESC;
+    if (op == 2 && d->r1.data && !view_ok(d->r1, d->ha, d->wa, 0, d->c, "bn.r1", 1)) return ISR_ERR_BAD_DESC;
+    if (op == 2 && d->r2.data && !view_ok(d->r2, d->ha, d->wa, 0, d->c, "bn.r2", 1)) return ISR_ERR_BAD_DESC;
+    if (op == 4 && d->dz.data && !view_ok(d->dz, d->ha, d->wa, 0, d->c, "bn.dz", 1)) return ISR_ERR_BAD_DESC;
+    if ((op == 2 || op == 4) && (!d->gamma || (op == 2 && !d->beta)))
+        return fail(ISR_ERR_BAD_DESC, "bn: null gamma / beta");
+    if (op == 1 && (!d->running_mean) != (!d->running_var)) return fail(ISR_ERR_BAD_DESC, "bn: running stats pair");
+    return ISR_OK;
+}
+
+static int bn_run(const isr_bn_desc* d, int op, isr_stream_t s, const char* what) {
+    int rc = bn_validate(d, op);
+    if (rc != ISR_OK) return rc;
+    return launched(isr::bn_dispatch(d, op, (hipStream_t)s), what);
+}
+
+int isr_bn_stats(const isr_bn_desc* d, isr_stream_t s) { return bn_run(d, 0, s, "bn_stats"); }
+int isr_bn_finalize(const isr_bn_desc* d, isr_stream_t s) { return bn_run(d, 1, s, "bn_finalize"); }
+int isr_bn_apply(const isr_bn_desc* d, isr_stream_t s) { return bn_run(d, 2, s, "bn_apply"); }
+int isr_bn_bwd_reduce(const isr_bn_desc* d, isr_stream_t s) { return bn_run(d, 3, s, "bn_bwd_reduce"); }
+int isr_bn_bwd_apply(const isr_bn_desc* d, isr_stream_t s) { return bn_run(d, 4, s, "bn_bwd_apply"); }
 
 }  // extern "C"

@@ -202,3 +202,180 @@ int maxpool2_dispatch(const isr_pool_desc* d, int backward, hipStream_t s) {
 }
 
 }  // namespace isr
+
+// ------------------------------------------------------------------ BatchNorm
+// Train-mode BatchNorm2d on channel-blocked views (the `bn` of Conv,
+// utils/models.py:75-111, in ResNet's train mode).  Statistics over (N, H, W)
+// per channel accumulate in double (caller-zeroed acc[2][c]); the per-thread
+// and per-block partials are fp32 over at most a few thousand values.
+namespace isr {
+
+constexpr int BN_ROWS = 8;  // rows of one plane per block
+
+// (sum, sumsq) of z  [mode 0]  or  (sum g, sum g*xhat) [mode 1] per channel
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_reduce_kernel(isr_bn_desc d) {
+    __shared__ float red[4][2][16];
+    const int planes = d.c / 16;
+    const int nrb = (d.h + BN_ROWS - 1) / BN_ROWS;
+    int b = blockIdx.x;
+    const int rb = b % nrb; b /= nrb;
+    const int pl = b % planes;
+    const int img = b / planes;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int half = threadIdx.x & 1;
+    const int c0 = pl * 16 + half * 8;
+    float s1[8], s2[8], mean[8], istd[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s1[k] = 0.f;
+        s2[k] = 0.f;
+        if (MODE == 1) { mean[k] = d.save[c0 + k]; istd[k] = d.save[d.c + c0 + k]; }
+    }
+    const int y0 = rb * BN_ROWS, y1 = min(d.h, y0 + BN_ROWS);
+    for (int y = y0; y < y1; ++y) {
+        for (int x = threadIdx.x >> 1; x < d.w; x += 128) {
+            float z[8];
+            load8_bf16(view_at(d.z, img, y, x, c0), z);
+            if (MODE == 0) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { s1[k] += z[k]; s2[k] += z[k] * z[k]; }
+            } else {
+                float g[8];
+                load8_bf16(view_at(d.y, img, y, x, c0), g);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { s1[k] += g[k]; s2[k] += g[k] * (z[k] - mean[k]) * istd[k]; }
+            }
+        }
+    }
+    // reduce over the 32 lanes of equal parity
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int o = 2; o < 64; o <<= 1) {
+            s1[k] += __shfl_xor(s1[k], o);
+            s2[k] += __shfl_xor(s2[k], o);
+        }
+    }
+    if (lane < 2) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { red[wave][0][half * 8 + k] = s1[k]; red[wave][1][half * 8 + k] = s2[k]; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        const int q = threadIdx.x >> 4, ch = threadIdx.x & 15;
+        const float v = red[0][q][ch] + red[1][q][ch] + red[2][q][ch] + red[3][q][ch];
+        atomicAdd(d.acc + q * d.c + pl * 16 + ch, (double)v);
+    }
+}
+
+// forward finalize: save = (mean, invstd); running stats (unbiased var), as nn.BatchNorm2d.train()
+__global__ void bn_finalize_kernel(isr_bn_desc d) {
+    const double cnt = (double)d.n * d.h * d.w;
+    for (int c = threadIdx.x; c < d.c; c += blockDim.x) {
+        const double mean = d.acc[c] / cnt;
+        double var = d.acc[d.c + c] / cnt - mean * mean;
+        var = var > 0.0 ? var : 0.0;
+        d.save[c] = (float)mean;
+        d.save[d.c + c] = (float)(1.0 / sqrt(var + (double)d.eps));
+        if (d.running_mean) {
+            d.running_mean[c] = (1.f - d.momentum) * d.running_mean[c] + d.momentum * (float)mean;
+            d.running_var[c] = (1.f - d.momentum) * d.running_var[c] + d.momentum * (float)(var * cnt / (cnt > 1 ? cnt - 1 : 1));
+        }
+    }
+}
+
+// y = ((act(a*z + b)) * s1 + r1) * s2 + r2;  a = gamma*invstd, b = beta - mean*a
+__global__ __launch_bounds__(256) void bn_apply_kernel(isr_bn_desc d) {
+    const int cg = d.c / 8;
+    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        size_t r = i;
+        const int half = r % 2; r /= 2;
+        const int x = r % d.wa; r /= d.wa;
+        const int y = r % d.ha; r /= d.ha;
+        const int pl = r % (d.c / 16);
+        const int img = (int)(r / (d.c / 16));
+        const int c = pl * 16 + half * 8;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (y < d.h && x < d.w) {
+            load8_bf16(view_at(d.z, img, y, x, c), v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float a = d.gamma[c + k] * d.save[d.c + c + k];
+                const float bb = d.beta[c + k] - d.save[c + k] * a;
+                float t = v[k] * a + bb;
+                t = t >= 0.f ? t : t * d.slope;
+                v[k] = t * d.s1;
+            }
+            if (d.r1.data) {
+                float t[8];
+                load8_bf16(view_at(d.r1, img, y, x, c), t);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] += t[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] *= d.s2;
+            if (d.r2.data) {
+                float t[8];
+                load8_bf16(view_at(d.r2, img, y, x, c), t);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] += t[k];
+            }
+        }
+        store8_bf16(view_at(d.y, img, y, x, c), v);
+    }
+}
+
+// dz = gscale * a * (g - sum(g)/N - xhat * sum(g*xhat)/N), in place over y; dgamma/dbeta
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(isr_bn_desc d) {
+    const int cg = d.c / 8;
+    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
+    const double cnt = (double)d.n * d.h * d.w;
+    if (blockIdx.x == 0) {
+        for (int c = threadIdx.x; c < d.c; c += blockDim.x) {
+            if (d.dgamma) d.dgamma[c] = (float)(d.acc[d.c + c]) * d.gscale;
+            if (d.dbeta) d.dbeta[c] = (float)(d.acc[c]) * d.gscale;
+        }
+    }
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        size_t r = i;
+        const int half = r % 2; r /= 2;
+        const int x = r % d.wa; r /= d.wa;
+        const int y = r % d.ha; r /= d.ha;
+        const int pl = r % (d.c / 16);
+        const int img = (int)(r / (d.c / 16));
+        const int c = pl * 16 + half * 8;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (y < d.h && x < d.w) {
+            float z[8], g[8];
+            load8_bf16(view_at(d.z, img, y, x, c), z);
+            load8_bf16(view_at(d.y, img, y, x, c), g);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float mean = d.save[c + k], istd = d.save[d.c + c + k];
+                const float mg = (float)(d.acc[c + k] / cnt), mgx = (float)(d.acc[d.c + c + k] / cnt);
+                const float xh = (z[k] - mean) * istd;
+                v[k] = d.gscale * d.gamma[c + k] * istd * (g[k] - mg - xh * mgx);
+            }
+        }
+        store8_bf16(view_at(d.dz.data ? d.dz : d.y, img, y, x, c), v);
+    }
+}
+
+int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s) {
+    const size_t total = (size_t)d->n * d->ha * d->wa * (d->c / 8);
+    const int ew_blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    const int red_blocks = d->n * (d->c / 16) * ((d->h + BN_ROWS - 1) / BN_ROWS);
+    switch (op) {
+        case 0: hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(red_blocks), dim3(256), 0, s, *d); break;
+        case 1: hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(256), 0, s, *d); break;
+        case 2: hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks), dim3(256), 0, s, *d); break;
+        case 3: hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(red_blocks), dim3(256), 0, s, *d); break;
+        case 4: hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks), dim3(256), 0, s, *d); break;
+        default: return -2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace isr

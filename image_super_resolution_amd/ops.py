@@ -420,3 +420,53 @@ def maxpool2_fwd(x: ActBuffer, y: ActBuffer, c: int) -> None:
 
 def maxpool2_bwd(x: ActBuffer, gy: ActBuffer, gx: ActBuffer, c: int, mslope: float = 0.0) -> None:
     check(_lib.load().isr_maxpool2_bwd(ctypes.byref(pool_desc(x, gy, c, gx, mslope)), _stream()), "isr_maxpool2_bwd")
+
+
+# ---------------------------------------------------------------- BatchNorm (train mode)
+class BNState:
+    """Per-layer scratch of the train-mode BatchNorm kernels: double accumulators
+    acc[2][c] and the saved (mean, invstd)[2][c]."""
+
+    def __init__(self, c: int, device):
+        self.c = c
+        self.acc = torch.zeros(2 * c, dtype=torch.float64, device=device)
+        self.save = torch.zeros(2 * c, dtype=torch.float32, device=device)
+
+
+def bn_desc(z: ActBuffer, y: ActBuffer, c: int, st: BNState, bn: "torch.nn.BatchNorm2d", *, z_coff: int = 0,
+            y_coff: int = 0, slope: float = 1.0, r1: ActBuffer | None = None, r1_coff: int = 0, s1: float = 1.0,
+            r2: ActBuffer | None = None, r2_coff: int = 0, s2: float = 1.0, dz: ActBuffer | None = None,
+            dz_coff: int = 0, dgamma: torch.Tensor | None = None, dbeta: torch.Tensor | None = None,
+            gscale: float = 1.0, update_running: bool = True) -> _lib.IsrBnDesc:
+    d = _lib.IsrBnDesc()
+    d.n, d.h, d.w, d.ha, d.wa, d.c = z.n, z.h, z.w, z.ha, z.wa, c
+    d.z, d.y = z.view(z_coff), y.view(y_coff)
+    d.r1 = r1.view(r1_coff) if r1 is not None else _NULL_VIEW
+    d.r2 = r2.view(r2_coff) if r2 is not None else _NULL_VIEW
+    d.dz = dz.view(dz_coff) if dz is not None else _NULL_VIEW
+    d.s1, d.s2, d.slope = s1, s2, slope
+    d.gamma, d.beta = bn.weight.data_ptr(), bn.bias.data_ptr()
+    if update_running and bn.running_mean is not None:
+        d.running_mean, d.running_var = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
+    d.momentum = float(bn.momentum if bn.momentum is not None else 0.1)
+    d.eps = float(bn.eps)
+    d.acc, d.save = st.acc.data_ptr(), st.save.data_ptr()
+    d.dgamma = dgamma.data_ptr() if dgamma is not None else None
+    d.dbeta = dbeta.data_ptr() if dbeta is not None else None
+    d.gscale = gscale
+    return d
+
+
+def bn_forward(d: _lib.IsrBnDesc, st: BNState) -> None:
+    lib, s = _lib.load(), _stream()
+    st.acc.zero_()
+    check(lib.isr_bn_stats(ctypes.byref(d), s), "isr_bn_stats")
+    check(lib.isr_bn_finalize(ctypes.byref(d), s), "isr_bn_finalize")
+    check(lib.isr_bn_apply(ctypes.byref(d), s), "isr_bn_apply")
+
+
+def bn_backward(d: _lib.IsrBnDesc, st: BNState) -> None:
+    lib, s = _lib.load(), _stream()
+    st.acc.zero_()
+    check(lib.isr_bn_bwd_reduce(ctypes.byref(d), s), "isr_bn_bwd_reduce")
+    check(lib.isr_bn_bwd_apply(ctypes.byref(d), s), "isr_bn_bwd_apply")

@@ -212,6 +212,39 @@ typedef struct isr_pool_desc {
 int isr_maxpool2_fwd(const isr_pool_desc* d, isr_stream_t s);
 int isr_maxpool2_bwd(const isr_pool_desc* d, isr_stream_t s);
 
+/* Train-mode BatchNorm2d (the `bn` of Conv, utils/models.py:75-111, trained by
+ * train.py with ResNet; nn.BatchNorm2d semantics: biased batch variance for the
+ * normalisation, unbiased for running_var, momentum update), on channel-blocked
+ * views of c channels.  Statistics accumulate in acc[2][c] (double, caller-zeroed
+ * before each reduce); finalize writes save[2][c] = (mean, 1/sqrt(var + eps)).
+ *   isr_bn_stats      acc += (sum z, sum z^2)
+ *   isr_bn_finalize   save, running_mean / running_var update
+ *   isr_bn_apply      y = ((LeakyReLU_slope(a z + b)) * s1 + r1) * s2 + r2,  a = gamma * invstd,
+ *                     b = beta - mean * a  (r1 / r2 optional; zero outside the valid region)
+ *   isr_bn_bwd_reduce acc += (sum g, sum g * xhat),  g = y view (gradient wrt the BN output)
+ *   isr_bn_bwd_apply  dz = gscale * a * (g - mean(g) - xhat * mean(g xhat))  into dz (or over y when
+ *                     dz.data == NULL); dgamma = gscale * sum(g xhat), dbeta = gscale * sum(g) */
+typedef struct isr_bn_desc {
+    int32_t n, h, w, ha, wa, c;
+    isr_view z, y, r1, r2, dz;
+    float s1, s2, slope;
+    const float* gamma;
+    const float* beta;
+    float* running_mean;      /* NULL: no running-stat update */
+    float* running_var;
+    float momentum, eps;
+    double* acc;
+    float* save;
+    float* dgamma;
+    float* dbeta;
+    float gscale;
+} isr_bn_desc;
+int isr_bn_stats(const isr_bn_desc* d, isr_stream_t s);
+int isr_bn_finalize(const isr_bn_desc* d, isr_stream_t s);
+int isr_bn_apply(const isr_bn_desc* d, isr_stream_t s);
+int isr_bn_bwd_reduce(const isr_bn_desc* d, isr_stream_t s);
+int isr_bn_bwd_apply(const isr_bn_desc* d, isr_stream_t s);
+
 /* Weight packing (device fp32 OIHW → device bf16 kernel layout).  Replaces the
  * one-off fuse step's weight preparation (utils/models.py:741-751); BN folding
  * itself is done by the caller before packing. */

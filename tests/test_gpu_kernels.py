@@ -367,3 +367,46 @@ def test_tail_dgrad_via_head_kernel_with_mask():
     torch.cuda.synchronize()
     ref = U.grad * torch.where(bf(act) > 0, 1.0, 0.01)
     close(out.to_nchw(), ref)
+
+
+@pytest.mark.parametrize("n,c,h,w,slope", [(2, 32, 20, 36, 0.01), (4, 64, 16, 32, 1.0), (1, 32, 7, 45, 0.01)])
+def test_batchnorm_train_forward_backward(n, c, h, w, slope):
+    """Train-mode BatchNorm2d kernels vs F.batch_norm(training=True) + autograd."""
+    from image_super_resolution_amd import ops
+    z = bf(_mk(n, c, h, w, 101) * 0.7 + 0.3)
+    bn = torch.nn.BatchNorm2d(c).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(c, device=DEV) + 0.5)
+        bn.bias.copy_(torch.randn(c, device=DEV) * 0.1)
+        bn.running_mean.copy_(torch.randn(c, device=DEV) * 0.1)
+        bn.running_var.copy_(torch.rand(c, device=DEV) + 0.5)
+    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
+    r = bf(_mk(n, c, h, w, 102))
+    zb = ops.ActBuffer.from_nchw(z, pad=1)
+    rb = ops.ActBuffer.from_nchw(r, pad=1)
+    yb = ops.ActBuffer.alloc(n, h, w, c, 1, DEV)
+    st = ops.BNState(c, DEV)
+    ops.bn_forward(ops.bn_desc(zb, yb, c, st, bn, slope=slope, r1=rb, s1=0.2, s2=0.5), st)
+    torch.cuda.synchronize()
+    zr = z.clone().requires_grad_(True)
+    w_ = bn.weight.detach().clone().requires_grad_(True)
+    b_ = bn.bias.detach().clone().requires_grad_(True)
+    pre = F.batch_norm(zr, rm, rv, w_, b_, training=True, momentum=0.1, eps=1e-5)
+    ref = (lrelu(pre, slope) * 0.2 + r) * 0.5
+    close(yb.to_nchw(), ref)
+    assert yb.outside_valid().float().abs().max().item() == 0.0
+    torch.testing.assert_close(bn.running_mean, rm, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, rv, rtol=1e-4, atol=1e-5)
+    # backward of the BN output (pre-activation gradient g), scaled
+    g = bf(_mk(n, c, h, w, 103))
+    pre.backward(g * 0.25)
+    gb = ops.ActBuffer.from_nchw(g, pad=1)
+    dzb = ops.ActBuffer.alloc(n, h, w, c, 1, DEV)
+    dgam = torch.empty(c, device=DEV)
+    dbet = torch.empty(c, device=DEV)
+    ops.bn_backward(ops.bn_desc(zb, gb, c, st, bn, dz=dzb, dgamma=dgam, dbeta=dbet, gscale=0.25), st)
+    torch.cuda.synchronize()
+    close(dzb.to_nchw(), zr.grad)
+    torch.testing.assert_close(dgam, w_.grad, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(dbet, b_.grad, rtol=2e-3, atol=2e-3)
+    assert torch.equal(gb.to_nchw(), g)  # dz went to its own buffer
