@@ -19,7 +19,12 @@ in reverse with three rotating 192-channel gradient buffers:
           the activation backward are both epilogue work
   trunk   g_f0 = chain + g_T, LeakyReLU'(f0) (ew_combine);  head wgrad9x9
 
-BatchNorm in train mode (ResNet) is not implemented on this path yet.
+ResNet's Conv layers carry train-mode BatchNorm (utils/models.py:75-111): the
+conv writes its pre-BN output z into a per-RDB z buffer, the BN kernels
+(isr_bn_*) reduce batch statistics, update the running stats and apply
+BN + activation (+ residuals) into the dense buffer; in the backward the BN
+input gradient is formed in place on the masked slot gradient before that
+conv's wgrad/dgrad, and dgamma/dbeta land in the flat gradient buffer.
 """
 from __future__ import annotations
 
@@ -48,6 +53,8 @@ class TConv:
     sub2: bool = False         # dgrad reads the PixelShuffle'd gradient (Scaler)
     fwd: torch.Tensor | None = None
     bwd: torch.Tensor | None = None
+    bn: nn.Module | None = None          # train-mode BatchNorm2d after the conv (ResNet's Conv)
+    bn_state: object | None = None
 
     def pack(self):
         w = self.w.detach()
@@ -65,23 +72,31 @@ class TConv:
         return self.b.detach() if self.b is not None else None
 
 
+def _bn_of(m: nn.Module):
+    bn = getattr(m, "bn", None)
+    return bn if isinstance(bn, nn.BatchNorm2d) else None
+
+
 def _generator_convs(gen: nn.Module) -> tuple[TConv, list[list[TConv]], TConv, list[TConv], TConv]:
-    """Conv layers of an EResNet in execution order (reference module paths)."""
-    def t(conv: nn.Conv2d, kind="3x3", **kw):
-        return TConv(conv.weight, conv.bias, conv.in_channels, conv.out_channels, kind, **kw)
+    """Conv layers of a ResNet / EResNet in execution order (reference module paths)."""
+    def t(m: nn.Module, kind="3x3", **kw):
+        conv = m.conv
+        return TConv(conv.weight, conv.bias, conv.in_channels, conv.out_channels, kind, bn=_bn_of(m), **kw)
 
     a = gen.add_rate
-    head = t(gen.conv0.conv, "head")
+    head = t(gen.conv0, "head")
     rdbs = []
     for i, rrdb in enumerate(gen.residual):
         for r, rdb in enumerate(rrdb.net):
-            # dgrad of the final conv carries the RDB (x add_rate) scale in the weights;
-            # the RRDB-level x add_rate of the third RDB is applied by the epilogue's s2
-            rdbs.append([t(rdb.conv0.conv), t(rdb.conv1.conv), t(rdb.conv2.conv), t(rdb.conv3.conv),
-                         t(rdb.conv.conv, dgrad_scale=a)])
-    conv1 = t(gen.conv1.conv)
-    scalers = [t(s.net[0].conv, sub2=True) for s in gen.scaler]
-    tail = t(gen.conv2.conv, "tail")
+            # without BN the dgrad of the final conv carries the RDB (x add_rate) scale in the
+            # weights (the RRDB-level x add_rate of the third RDB is the epilogue's s2); with BN
+            # the scale is applied by the BN backward (gscale) instead
+            fin = _bn_of(rdb.conv)
+            rdbs.append([t(rdb.conv0), t(rdb.conv1), t(rdb.conv2), t(rdb.conv3),
+                         t(rdb.conv, dgrad_scale=(1.0 if fin is not None else a))])
+    conv1 = t(gen.conv1)
+    scalers = [t(s.net[0], sub2=True) for s in gen.scaler]
+    tail = t(gen.conv2, "tail")
     return head, rdbs, conv1, scalers, tail
 
 
@@ -91,12 +106,11 @@ class GeneratorTrainPlan:
     gradients come back in the order of `params()`."""
 
     def __init__(self, gen: nn.Module, n: int, h: int, w: int, device):
-        from .models import EResNet, SRGAN
+        from .models import EResNet, ResNet, SRGAN
         if isinstance(gen, SRGAN):
             gen = gen.res_net
-        if not isinstance(gen, EResNet):
-            raise NotImplementedError("HIP training path: EResNet / SRGAN(enchant=True) generators "
-                                      "(ResNet's train-mode BatchNorm is not implemented yet)")
+        if not isinstance(gen, (EResNet, ResNet)):
+            raise NotImplementedError(f"HIP training path covers ResNet / EResNet / SRGAN, got {type(gen).__name__}")
         self.gen, self.key = gen, (n, h, w, str(device))
         self.device = torch.device(device)
         self.a = float(gen.add_rate)
@@ -121,12 +135,24 @@ class GeneratorTrainPlan:
         self.gT = ActBuffer.alloc(n, h, w, 64, 1, dev)
         self.gups = [ActBuffer.alloc(u.n, u.h, u.w, 64, 2, dev, ha=u.ha, wa=u.wa) for u in self.ups]
         self.gf0 = ActBuffer.alloc(n, h, w, 64, 1, dev)
-        # ---- parameters / gradient layout (one flat fp32 gradient buffer per backward)
         self.convs = [self.head] + [c for r in self.rdbs for c in r] + [self.conv1] + self.scalers + [self.tail]
+        # ---- train-mode BatchNorm (ResNet): pre-BN conv outputs z and per-layer BN scratch
+        self.has_bn = any(c.bn is not None for c in self.convs)
+        if self.has_bn:
+            self.Zb = [ActBuffer.alloc(n, h, w, 192, 1, dev) for _ in range(nr)]
+            self.Tz = ActBuffer.alloc(n, h, w, 64, 1, dev)
+            self.gtmp = ActBuffer.alloc(n, h, w, 64, 1, dev)
+            for c in self.convs:
+                if c.bn is not None:
+                    c.bn_state = ops.BNState(c.cout, dev)
+        self.bn_counters = [c.bn.num_batches_tracked for c in self.convs
+                            if c.bn is not None and c.bn.num_batches_tracked is not None]
+        # ---- parameters / gradient layout (one flat fp32 gradient buffer per backward)
         self._params, self._goff = [], []
         off = 0
         for c in self.convs:
-            for p in (c.w, c.b):
+            ps = [c.w, c.b] + ([c.bn.weight, c.bn.bias] if c.bn is not None else [])
+            for p in ps:
                 if p is not None:
                     self._params.append(p)
                     self._goff.append(off)
@@ -153,16 +179,25 @@ class GeneratorTrainPlan:
         F = []
         self.head_desc = ops.head9x9_desc(self.dummy_x, self.head.fwd, self.head.bias, f0, slope=self.slope0, y2=D[0])
         F.append((head, self.head_desc))
+        def conv_bn(x, cin, c, y, y_coff, z, z_coff, slope, **res):
+            """conv → y directly, or (BN layer) conv → z, batch stats, BN+act(+residuals) → y."""
+            if c.bn is None:
+                F.append((conv, ops.conv3x3_desc(x, cin, c.fwd, c.bias, c.cout, y, y_coff=y_coff, slope=slope, **res)))
+            else:
+                F.append((conv, ops.conv3x3_desc(x, cin, c.fwd, c.bias, c.cout, z, y_coff=z_coff, slope=1.0)))
+                F.append(("bnf", ops.bn_desc(z, y, c.cout, c.bn_state, c.bn, z_coff=z_coff, y_coff=y_coff,
+                                             slope=slope, **res), c.bn_state))
+
         for j, cs in enumerate(self.rdbs):
+            Zj = self.Zb[j] if self.has_bn else None
             for k in range(4):
                 c = cs[k]
-                F.append((conv, ops.conv3x3_desc(D[j], c.cin, c.fwd, c.bias, c.cout, D[j], y_coff=c.cin, slope=LEAKY)))
+                conv_bn(D[j], c.cin, c, D[j], c.cin, Zj, c.cin, LEAKY)
             c = cs[4]
             extra = dict(r2=D[j - 2], s2=a) if j % 3 == 2 else {}
-            F.append((conv, ops.conv3x3_desc(D[j], 192, c.fwd, c.bias, 64, D[j + 1], slope=1.0, r1=D[j], s1=a,
-                                             **extra)))
+            conv_bn(D[j], 192, c, D[j + 1], 0, Zj, 0, 1.0, r1=D[j], s1=a, **extra)
         c = self.conv1
-        F.append((conv, ops.conv3x3_desc(D[-1], 64, c.fwd, c.bias, 64, T, slope=1.0, r1=f0, s1=1.0)))
+        conv_bn(D[-1], 64, c, T, 0, self.Tz if self.has_bn else None, 0, 1.0, r1=f0, s1=1.0)
         cur = T
         for s, c in enumerate(self.scalers):
             F.append((conv, ops.conv3x3_desc(cur, 64, c.fwd, c.bias, 256, self.ups[s], slope=LEAKY, shuffle=2)))
@@ -197,11 +232,20 @@ class GeneratorTrainPlan:
             out = self.gups[s - 1] if s > 0 else self.gT
             kw = dict(m=self.ups[s - 1], mslope=LEAKY) if s > 0 else {}
             B.append(("conv", ops.conv3x3_desc(self.gups[s], 256, c.bwd, None, 64, out, x_sub2=True, **kw)))
-        # conv1:  T = conv1(D[-1][0:64]) + f0
+        def bn_bwd(c, z, g, *, z_coff=0, g_coff=0, dz=None, gscale=1.0):
+            """BN input gradient of conv c: g (gradient wrt the BN output) → dz (in place if dz is None)."""
+            B.append(("bnb", ops.bn_desc(z, g, c.cout, c.bn_state, c.bn, z_coff=z_coff, y_coff=g_coff, dz=dz,
+                                         gscale=gscale), ci[id(c)], c.bn_state))
+
+        # conv1:  T = BN?(conv1(D[-1][0:64])) + f0
         c = self.conv1
         U, V, W = self.G
-        wg3(D[-1], 64, self.gT, 64, c)
-        B.append(("conv", ops.conv3x3_desc(self.gT, 64, c.bwd, None, 64, U)))
+        g1 = self.gT
+        if c.bn is not None:
+            bn_bwd(c, self.Tz, self.gT, dz=self.gtmp)
+            g1 = self.gtmp
+        wg3(D[-1], 64, g1, 64, c)
+        B.append(("conv", ops.conv3x3_desc(g1, 64, c.bwd, None, 64, U)))
         # RRDBs, reverse
         nb = len(self.rdbs) // 3
         for i in range(nb - 1, -1, -1):
@@ -213,12 +257,22 @@ class GeneratorTrainPlan:
                 c5 = cs[4]
                 last_rdb = step == 0  # the third RDB of the RRDB (first in reverse)
                 # final conv: out = conv*a + Dj[0:64]  (third RDB: (...)*a + RRDB input)
-                wg3(Dj, 192, gin, 64, c5, scale=(a * a if last_rdb else a))
-                B.append(("conv", ops.conv3x3_desc(gin, 64, c5.bwd, None, 192, gout, r1=gin, r1_cn=64,
-                                                   s2=(a if last_rdb else 1.0), m=Dj, m_c0=160, mslope=LEAKY)))
+                res = a if last_rdb else 1.0       # coefficient of Dj[0:64] in the RRDB output
+                if c5.bn is None:
+                    wg3(Dj, 192, gin, 64, c5, scale=(a * a if last_rdb else a))
+                    B.append(("conv", ops.conv3x3_desc(gin, 64, c5.bwd, None, 192, gout, r1=gin, r1_cn=64,
+                                                       s2=res, m=Dj, m_c0=160, mslope=LEAKY)))
+                else:
+                    # dz5 = BN'(a*res * g_R) into gtmp; residual keeps g_R: y = (v/res + g_R) * res
+                    bn_bwd(c5, self.Zb[j], gin, dz=self.gtmp, gscale=a * res)
+                    wg3(Dj, 192, self.gtmp, 64, c5)
+                    B.append(("conv", ops.conv3x3_desc(self.gtmp, 64, c5.bwd, None, 192, gout, r1=gin, r1_cn=64,
+                                                       s1=1.0 / res, s2=res, m=Dj, m_c0=160, mslope=LEAKY)))
                 for k in range(3, -1, -1):
                     ck = cs[k]
                     slot = 64 + 32 * k
+                    if ck.bn is not None:  # slot k is complete and LeakyReLU'-masked: BN backward in place
+                        bn_bwd(ck, self.Zb[j], gout, z_coff=slot, g_coff=slot)
                     wg3(Dj, ck.cin, gout, 32, ck, g_coff=slot)
                     kw = dict(m=Dj, m_c0=slot - 32, mslope=LEAKY) if k > 0 else {}
                     if k == 0 and step == 2:
@@ -245,7 +299,7 @@ class GeneratorTrainPlan:
             raise RuntimeError("train plan: could not size the wgrad workspace: "
                                + lib.isr_last_error().decode(errors="replace"))
         self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        # gradient offsets per conv: (w offset, b offset or None)
+        # gradient offsets per conv: (w, b or None, bn weight or None, bn bias or None)
         self._conv_goff = []
         pi = 0
         for c in self.convs:
@@ -255,7 +309,11 @@ class GeneratorTrainPlan:
             if c.b is not None:
                 bo = self._goff[pi]
                 pi += 1
-            self._conv_goff.append((wo, bo))
+            go = bo2 = None
+            if c.bn is not None:
+                go, bo2 = self._goff[pi], self._goff[pi + 1]
+                pi += 2
+            self._conv_goff.append((wo, bo, go, bo2))
 
     # -------------------------------------------------------------- execution
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -270,10 +328,21 @@ class GeneratorTrainPlan:
         self.head_wg.p = x.data_ptr()
         st = ops._stream()
         byref = ctypes.byref
-        for fn, d in self.fwd_launches:
-            rc = fn(byref(d), st)
+        lib = self.lib
+        for e in self.fwd_launches:
+            if e[0] == "bnf":
+                d, bst = e[1], e[2]
+                bst.acc.zero_()
+                for fn in (lib.isr_bn_stats, lib.isr_bn_finalize, lib.isr_bn_apply):
+                    rc = fn(byref(d), st)
+                    if rc != 0:
+                        ops.check(rc, "train forward (bn)")
+                continue
+            rc = e[0](byref(e[1]), st)
             if rc != 0:
                 ops.check(rc, "train forward")
+        if self.bn_counters:
+            torch._foreach_add_(self.bn_counters, 1)  # nn.BatchNorm2d.train() bookkeeping
         self.y = y
         return y
 
@@ -288,8 +357,15 @@ class GeneratorTrainPlan:
             kind, d = e[0], e[1]
             if kind == "conv":
                 rc = lib.isr_conv3x3_fwd(byref(d), st)
+            elif kind == "bnb":
+                _, _, go, bo2 = self._conv_goff[e[2]]
+                d.dgamma, d.dbeta = gbase + 4 * go, gbase + 4 * bo2
+                e[3].acc.zero_()
+                rc = lib.isr_bn_bwd_reduce(byref(d), st)
+                if rc == 0:
+                    rc = lib.isr_bn_bwd_apply(byref(d), st)
             elif kind == "wg3" or kind == "wg9":
-                wo, bo = self._conv_goff[e[2]]
+                wo, bo = self._conv_goff[e[2]][:2]
                 d.dw = gbase + 4 * wo
                 d.db = gbase + 4 * bo if bo is not None else None
                 rc = (lib.isr_wgrad3x3 if kind == "wg3" else lib.isr_wgrad9x9)(byref(d), ws, wsn, st)

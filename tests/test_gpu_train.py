@@ -85,3 +85,57 @@ def test_train_step_updates_and_repacks():
         lr_.backward()
         opt_ref.step()
         assert abs(l.item() - lr_.item()) <= 2e-3 * abs(lr_.item()), (l.item(), lr_.item())
+
+
+def test_resnet_train_step_vs_reference_golden(golden):
+    """ResNet (train-mode BatchNorm) step vs the reference's own fp32 outputs
+    (tests/golden/train_step_x2.npz): prediction, MSE loss, a spread of
+    parameter gradients (conv, BN weight/bias, scaler, tail) and BN running stats."""
+    g = golden("train_step_x2")
+    m = models.ResNet(1, 0.2, scaleRate=2)
+    m.load_state_dict(synth_state_dict(m.state_dict(), int(g["seed"])))
+    m = m.to(DEV).train()
+    pred = m(torch.from_numpy(g["x"]).to(DEV))
+    loss = F.mse_loss(pred, torch.from_numpy(g["target"]).to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    ref_pred = torch.from_numpy(g["pred"]).to(DEV)
+    assert R.psnr(pred.detach().cpu(), ref_pred.cpu()) >= 40.0
+    assert abs(loss.item() - float(g["loss"])) <= 1e-2 * float(g["loss"])
+    params = dict(m.named_parameters())
+    for k in g:
+        if k.startswith("grad:"):
+            got, ref = params[k[5:]].grad, torch.from_numpy(g[k]).to(DEV)
+            rel = ((got - ref).norm() / ref.norm()).item()
+            cos = F.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
+            assert rel <= 5e-2 and cos >= 0.998, f"{k}: rel {rel:.3e} cos {cos:.5f}"
+    bufs = dict(m.named_buffers())
+    for k in g:
+        if k.startswith("stat:"):
+            got, ref = bufs[k[5:]], torch.from_numpy(g[k]).to(DEV)
+            assert ((got - ref).norm() / ref.norm()).item() <= 1e-2, k
+    assert int(bufs["residual.0.net.0.conv0.bn.num_batches_tracked"].item()) == 1
+
+
+def test_resnet_train_step_all_grads_vs_oracle():
+    m = models.ResNet(2, 0.2, scaleRate=4)
+    m.load_state_dict(synth_state_dict(m.state_dict(), 9))
+    lr, hr01 = synth_lr_batch(2, 20, 24, seed=21, scale=4)
+    x, hr = normalize(lr), hr01 * 2 - 1
+    sd = {k: v.detach().clone().float() for k, v in m.state_dict().items()}
+    params = {k: v.requires_grad_(True) for k, v in sd.items() if v.is_floating_point() and "running" not in k}
+    y_ref = R.generator(sd, x, num_blocks=2, scale=4, train_bn=True)
+    F.mse_loss(y_ref, hr).backward()
+    m = m.to(DEV).train()
+    F.mse_loss(m(x.to(DEV)), hr.to(DEV)).backward()
+    for name, p in m.named_parameters():
+        r = params[name].grad.to(DEV)
+        rel = ((p.grad - r).norm() / r.norm().clamp_min(1e-12)).item()
+        cos = F.cosine_similarity(p.grad.flatten(), r.flatten(), dim=0).item()
+        # BN gamma/beta gradients are batch sums of bf16 slot gradients with heavy
+        # cancellation: 10 % / 0.995; conv weights 5 % / 0.998
+        lim_rel, lim_cos = (0.1, 0.995) if ".bn." in name else (5e-2, 0.998)
+        assert rel <= lim_rel and cos >= lim_cos, f"{name}: rel {rel:.3e} cos {cos:.5f}"
+    for name, b in m.named_buffers():
+        if "running" in name:
+            torch.testing.assert_close(b.cpu(), sd[name], rtol=1e-2, atol=1e-3)
