@@ -189,15 +189,18 @@ class GeneratorPlan:
         self.launches = L
         self._keep = (dummy_x, dummy_out)
 
-    def run(self, x: torch.Tensor, out: torch.Tensor, around=None) -> torch.Tensor:
-        """Launch the forward on the current stream.  `around(tag)` may return
-        (start_event, end_event) to bracket that launch."""
+    def bind(self, x: torch.Tensor, out: torch.Tensor) -> None:
         if tuple(out.shape) != self.out_shape or out.dtype != self.out_dtype or not out.is_contiguous():
             raise ValueError("GeneratorPlan.run: output tensor does not match the plan")
         if not x.is_contiguous():
             raise ValueError("GeneratorPlan.run: input must be contiguous NCHW")
         self.head_desc.x = x.data_ptr()
         self.tail_desc.y = out.data_ptr()
+
+    def run(self, x: torch.Tensor, out: torch.Tensor, around=None) -> torch.Tensor:
+        """Launch the forward on the current stream.  `around(tag)` may return
+        (start_event, end_event) to bracket that launch."""
+        self.bind(x, out)
         stream = ops._stream()
         byref = ctypes.byref
         cv = self._conv_variant
@@ -211,6 +214,70 @@ class GeneratorPlan:
             if ev is not None:
                 ev[1].record()
         return out
+
+
+class SplitGeneratorPlan:
+    """The batch split into `splits` equal sub-batches, each with its own buffers
+    and launch list on its own HIP stream; launches are issued interleaved
+    (layer i of every sub-batch, then layer i+1).  Sub-batch k > 0 starts
+    `stagger_us * k` later, so that one sub-batch's epilogue (HBM-bound) runs
+    beside another's main loop (MFMA-bound) on the same CUs."""
+
+    def __init__(self, gw: GeneratorWeights, n: int, h: int, w: int, device, x_u8: bool, out_u8: bool,
+                 mean, std, splits: int = 2, stagger_us: float = 0.0, variants: dict | None = None):
+        if n % splits:
+            raise ValueError(f"batch {n} does not split into {splits} equal sub-batches")
+        self.m = n // splits
+        self.key = (n, h, w, str(device), x_u8, out_u8, tuple(mean), tuple(std), splits, stagger_us)
+        self.subs = [GeneratorPlan(gw, self.m, h, w, device, x_u8, out_u8, mean, std, variants=variants)
+                     for _ in range(splits)]
+        self.out_shape = (n,) + self.subs[0].out_shape[1:]
+        self.out_dtype = self.subs[0].out_dtype
+        self.streams = [torch.cuda.Stream(device) for _ in range(splits)]
+        self._sp = [ctypes.c_void_p(s.cuda_stream) for s in self.streams]
+        self.stagger_cycles = int(stagger_us * _sleep_cycles_per_us()) if stagger_us > 0 else 0
+
+    def run(self, x: torch.Tensor, out: torch.Tensor, around=None) -> torch.Tensor:
+        if tuple(out.shape) != self.out_shape or out.dtype != self.out_dtype or not out.is_contiguous():
+            raise ValueError("SplitGeneratorPlan.run: output tensor does not match the plan")
+        m = self.m
+        for k, p in enumerate(self.subs):
+            p.bind(x[k * m:(k + 1) * m], out[k * m:(k + 1) * m])
+        cur = torch.cuda.current_stream()
+        for k, s in enumerate(self.streams):
+            s.wait_stream(cur)
+            if k and self.stagger_cycles:
+                with torch.cuda.stream(s):
+                    torch.cuda._sleep(self.stagger_cycles * k)
+        byref = ctypes.byref
+        cv = self.subs[0]._conv_variant
+        lists = [p.launches for p in self.subs]
+        for i in range(len(lists[0])):
+            for k, L in enumerate(lists):
+                fn, d, tag, var = L[i]
+                rc = fn(byref(d), self._sp[k]) if var is None else cv(byref(d), var, self._sp[k])
+                if rc != 0:
+                    ops.check(rc, f"{tag[0]} launch")
+        for s in self.streams:
+            cur.wait_stream(s)
+        return out
+
+
+_SLEEP_CAL: list[float] = []
+
+
+def _sleep_cycles_per_us() -> float:
+    """torch.cuda._sleep spins on the device clock; calibrate cycles per µs once."""
+    if not _SLEEP_CAL:
+        cyc = 2_000_000
+        torch.cuda._sleep(cyc)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.cuda._sleep(cyc)
+        e1.record()
+        torch.cuda.synchronize()
+        _SLEEP_CAL.append(cyc / (e0.elapsed_time(e1) * 1e3))
+    return _SLEEP_CAL[0]
 
 
 def get_plan(gw: GeneratorWeights, x: torch.Tensor, out_u8: bool, mean, std) -> GeneratorPlan:

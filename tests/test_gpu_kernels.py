@@ -166,10 +166,12 @@ def test_tail9x9(u8):
 
 def test_bad_descriptor_raises():
     from image_super_resolution_amd import ops, _lib
-    x = ops.ActBuffer.alloc(1, 16, 32, 48, 1, DEV)  # cin 48 not a multiple of 32
+    x = ops.ActBuffer.alloc(1, 16, 32, 48, 1, DEV)
     y = ops.ActBuffer.alloc(1, 16, 32, 64, 1, DEV)
-    with pytest.raises(_lib.IsrError, match="multiple of 32"):
-        ops.conv3x3(x, 48, torch.zeros(10, dtype=torch.bfloat16, device=DEV), None, 64, y)
+    with pytest.raises(_lib.IsrError, match="multiple of 16"):  # cin 40: not a whole K-step
+        ops.conv3x3(x, 40, torch.zeros(10, dtype=torch.bfloat16, device=DEV), None, 64, y)
+    with pytest.raises(_lib.IsrError, match="multiple of 32"):  # cout 48: not a whole MFMA tile
+        ops.conv3x3(x, 48, torch.zeros(10, dtype=torch.bfloat16, device=DEV), None, 48, y)
 
 
 def test_conv3x3_backward_epilogue_mask_and_limited_residual():

@@ -16,7 +16,15 @@ from image_super_resolution_amd import models
 from image_super_resolution_amd.weights import synth_state_dict
 from oracle import ref_cpu as R
 
-torch.set_grad_enabled(False)
+
+@pytest.fixture(autouse=True)
+def _no_grad():
+    """Grad off for this module's tests only (a module-level set_grad_enabled(False)
+    would leak into every test collected after it)."""
+    prev = torch.is_grad_enabled()
+    torch.set_grad_enabled(False)
+    yield
+    torch.set_grad_enabled(prev)
 
 
 def _sd(model, seed):
