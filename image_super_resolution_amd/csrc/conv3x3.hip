@@ -24,10 +24,11 @@
 
 namespace isr {
 
-template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1)>
+template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1), int EPQ_ = 4>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
     static constexpr int PIPE = PIPE_; // 1: double-buffered fragment registers across (k-step, dx) steps
+    static constexpr int EPQ = EPQ_;   // epilogue operand units (8 VGPRs each) loaded per pass
     static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol)
     // Ablation bits, timing-only builds (outputs wrong): 1 = no MFMA (operands
     // kept live), 2 = stage only chunk 0 (no refill), 4 = no epilogue stores.
@@ -121,58 +122,79 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
         }
     } else {
         const int xx = x0 + l31;
+        // Residual / mask operands are loaded U (row, fragment) units at a time,
+        // all loads of a pass before any of its stores, so the epilogue waits
+        // for memory R*NF/U times instead of once per unit.  U is sized so the
+        // operand registers stay at <= 32 VGPRs beside the 128 accumulators.
+        // Loads of a unit precede its stores (in-place RRDB update: y may alias r1/r2).
+        constexpr int P = ((MODE & 1) ? 1 : 0) + ((MODE & 2) ? 1 : 0) + ((MODE & 16) ? 1 : 0);
+        constexpr int NU = R * NF;
+        constexpr int U0 = P == 0 ? 1 : (C::EPQ / P > 0 ? C::EPQ / P : 1);
+        constexpr int U = U0 > NU ? NU : U0;
+        static_assert(NU % U == 0, "units per pass");
+        bf16x8 q1[U][2], q2[U][2], qm[U][2];
+        auto load_unit = [&](int uu, int buf) {
+            const int r = uu / NF, f = uu % NF;
+            const int yy = y0 + wave * R + r;
+            const int cf = ct * CT + f * 32;
+            const bool use_r1 = (MODE & 1) && (d.r1_cn == 0 || cf < d.r1_cn);
+            const bool use_m = (MODE & 16) && cf >= d.m_c0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
+            for (int blk = 0; blk < 2; ++blk) {
+                const int co = cf + 16 * blk + 8 * hh;
+                if constexpr (MODE & 1) {
+                    if (use_r1) q1[buf][blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r1, img, yy, xx, co));
+                }
+                if constexpr (MODE & 2) q2[buf][blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r2, img, yy, xx, co));
+                if constexpr (MODE & 16) {
+                    if (use_m) qm[buf][blk] = *reinterpret_cast<const bf16x8*>(view_at(d.m, img, yy, xx, co));
+                }
+            }
+        };
+        const bool scale2 = d.s2 != 1.f;  // s2 also scales when there is no r2 (backward)
+#pragma unroll
+        for (int uu = 0; uu < NU; ++uu) {
+            const int r = uu / NF, f = uu % NF, cb = uu % U;
             const int yy = y0 + wave * R + r;
             const bool valid = yy < d.h && xx < d.w;
+            if constexpr (P > 0) {
+                if (cb == 0) {
 #pragma unroll
-            for (int f = 0; f < NF; ++f) {
-                bf16x8 q1[2], q2[2], qm[2]; // residuals / mask of this fragment, loaded before its stores
-                const int cf = ct * CT + f * 32;
-                const bool use_r1 = (MODE & 1) && (d.r1_cn == 0 || cf < d.r1_cn);
-                const bool use_m = (MODE & 16) && cf >= d.m_c0;
-                const bool scale2 = d.s2 != 1.f;  // s2 also scales when there is no r2 (backward)
+                    for (int i = 0; i < U; ++i) load_unit(uu + i, i);
+                }
+            }
+            const int cf = ct * CT + f * 32;
+            const bool use_r1 = (MODE & 1) && (d.r1_cn == 0 || cf < d.r1_cn);
+            const bool use_m = (MODE & 16) && cf >= d.m_c0;
+            float v[16];
 #pragma unroll
-                for (int blk = 0; blk < 2; ++blk) {
-                    const int co = cf + 16 * blk + 8 * hh;
-                    if constexpr (MODE & 1) {
-                        if (use_r1) q1[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r1, img, yy, xx, co));
+            for (int g = 0; g < 16; ++g) v[g] = acc[r][f][g];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                swap_halves(v[k], v[4 + k]);
+                swap_halves(v[8 + k], v[12 + k]);
+            }
+            // v[8*blk + e] = cout f*32 + 16*blk + 8*hh + e
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk) {
+                float* u = v + 8 * blk;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
+                    if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (use_r1 ? (float)q1[cb][blk][e] : 0.f);
+                    if constexpr (MODE & 2) {
+                        u[e] = u[e] * d.s2 + (float)q2[cb][blk][e];
+                    } else {
+                        if (scale2) u[e] *= d.s2;
                     }
-                    if constexpr (MODE & 2) q2[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r2, img, yy, xx, co));
                     if constexpr (MODE & 16) {
-                        if (use_m) qm[blk] = *reinterpret_cast<const bf16x8*>(view_at(d.m, img, yy, xx, co));
+                        if (use_m && !((float)qm[cb][blk][e] > 0.f)) u[e] *= d.mslope;
                     }
+                    if (!valid) u[e] = 0.f;
                 }
-                float v[16];
-#pragma unroll
-                for (int g = 0; g < 16; ++g) v[g] = acc[r][f][g];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    swap_halves(v[k], v[4 + k]);
-                    swap_halves(v[8 + k], v[12 + k]);
-                }
-                // v[8*blk + e] = cout f*32 + 16*blk + 8*hh + e
-#pragma unroll
-                for (int blk = 0; blk < 2; ++blk) {
-                    float* u = v + 8 * blk;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
-                        if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (use_r1 ? (float)q1[blk][e] : 0.f);
-                        if constexpr (MODE & 2) {
-                            u[e] = u[e] * d.s2 + (float)q2[blk][e];
-                        } else {
-                            if (scale2) u[e] *= d.s2;
-                        }
-                        if constexpr (MODE & 16) {
-                            if (use_m && !((float)qm[blk][e] > 0.f)) u[e] *= d.mslope;
-                        }
-                        if (!valid) u[e] = 0.f;
-                    }
-                    const int co = ct * CT + f * 32 + 16 * blk + 8 * hh;
-                    store8_bf16(view_at(d.y, img, yy, xx, co), u);
-                    if constexpr (MODE & 4) store8_bf16(view_at(d.y2, img, yy, xx, co), u);
-                }
+                const int co = cf + 16 * blk + 8 * hh;
+                store8_bf16(view_at(d.y, img, yy, xx, co), u);
+                if constexpr (MODE & 4) store8_bf16(view_at(d.y2, img, yy, xx, co), u);
             }
         }
     }
@@ -420,6 +442,7 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 5: return launch3x3<C3<4, 4, 1, 16, 2, 0, 2>>(d, s);
             case 6: return launch3x3<C3<4, 4, 1, 16, 2, 0, 4>>(d, s);
             case 7: return launch3x3<C3<4, 4, 1, 16, 2, 0, 3>>(d, s);
+            case 8: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 1>>(d, s);  // V_G0, one unit per epilogue pass
         }
         return -2;
     }
@@ -433,6 +456,8 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
         case 5: return launch3x3<C3<4, 4, 2, 16, 2, 0, 2>>(d, s);
         case 6: return launch3x3<C3<4, 4, 2, 16, 2, 0, 4>>(d, s);
         case 7: return launch3x3<C3<4, 4, 2, 16, 2, 0, 3>>(d, s);
+        case 8: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 0, 1>>(d, s)  // V_F0 / V_W0, one unit per pass
+                                     : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 1>>(d, s);
     }
     return -2;
 }

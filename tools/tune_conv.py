@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3")
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="", help="comma list of CINxCOUT shapes, e.g. 160x32,192x64")
+    ap.add_argument("--final-r1-only", action="store_true", help="192->64 with r1 only (RDB 1/2 final conv)")
     args = ap.parse_args()
     lib = _lib.load()
     dev = "cuda"
@@ -57,7 +58,8 @@ def main():
             kw = dict(y_coff=cin, slope=0.01)
         else:
             dst = ops.ActBuffer.alloc(n, s, s, 192, 1, dev)
-            kw = dict(slope=1.0, r1=src, s1=0.2, r2=src, s2=0.2) if cin == 192 else dict(slope=1.0)
+            kw = dict(slope=1.0) if cin != 192 else (dict(slope=1.0, r1=src, s1=0.2) if args.final_r1_only
+                                                       else dict(slope=1.0, r1=src, s1=0.2, r2=src, s2=0.2))
         d = ops.conv3x3_desc(src, cin, wp, b, cout, dst, **kw)
         stream = ops._stream()
         outs = {}
