@@ -13,7 +13,12 @@ dealt across ranks and rank 0 writes the image.
 `--model` takes a checkpoint written by this package's train.py (state_dicts,
 loaded with weights_only=True) or a state_dict / .safetensors file; the
 reference's TorchScript export is not executed.
-Video inputs (rs.py:54-76) need the ffmpeg binary and are not handled here.
+Video (rs.py:54-76, BASELINE cfg5): container formats are decoded / encoded by
+the ffmpeg binary through raw pipes (as the reference does); headerless rgb24
+input (.rgb, with --video_size WxH) and bgr24 output (.bgr / .raw save_dir) work
+without ffmpeg.  The per-batch forward is a captured HIP graph (video.py).
+
+    python rs.py --model ck.pt --src clip.mp4 --save_dir out.mp4 --batch_size 2
 """
 from __future__ import annotations
 
@@ -25,9 +30,10 @@ from pathlib import Path
 import numpy as np
 import torch
 
-from image_super_resolution_amd import checkpoint, models, tiler
+from image_super_resolution_amd import checkpoint, models, tiler, video
 
-VID_FORMATS = ('.mp4', '.avi', '.mkv', '.mov', '.wmv', '.flv', '.webm', '.mpeg', '.mpg', '.m4v', '.ts')
+VID_FORMATS = video.VID_FORMATS
+RAW_FORMATS = (".rgb", ".raw", ".rgb24")
 
 
 def read_image(path: Path) -> torch.Tensor:
@@ -51,10 +57,39 @@ def build_model(path: str, add_rate: float, mean, std) -> models.Model:
     return m.fuse().eval()
 
 
+def run_video(kw, device) -> None:
+    """rs.py:54-76: frames → HIP graph forward → BGR frames → recorder."""
+    src, result = Path(kw["src"]), Path(kw["save_dir"])
+    wh = kw.get("video_size")
+    w, h = (int(v) for v in wh.lower().split("x")) if wh else (None, None)
+    source = video.open_video(src, w, h, kw.get("fps") or 30.0)
+    model = build_model(kw["model"], kw["add_rate"], kw["mean"], kw["std"])
+    runner = tiler.runner_for(model, device)
+    up = video.FrameUpscaler(runner.gw, source.height, source.width, kw["batch_size"], runner.mean, runner.std,
+                             device)
+    H, W = up.out_hw
+    if result.suffix.lower() in (".bgr", ".raw"):
+        rec = video.RawRecorder(result, (W, H), source.fps)
+    else:
+        result = result.with_suffix(".mp4")
+        rec = video.FFMPEG_recorder(result.as_posix(), (W, H), source.fps)
+    t0 = time.perf_counter()
+    n = video.VideoUpscaler(up).run(source, rec)
+    rec.stopRecorder()
+    dt = time.perf_counter() - t0
+    if src.suffix.lower() in VID_FORMATS:
+        rec.addAudio(src.as_posix())
+    print(f"{n} frames {source.width}x{source.height} -> {W}x{H} in {dt:.2f}s ({n / dt:.2f} fps) -> {result}")
+
+
 def runer(**kw):
     src, result = Path(kw["src"]), Path(kw["save_dir"])
-    if src.suffix.lower() in VID_FORMATS:
-        raise NotImplementedError("video super-resolution (rs.py:54-76) needs ffmpeg, which this image lacks")
+    if src.suffix.lower() in VID_FORMATS + RAW_FORMATS:
+        if not torch.cuda.is_available():
+            raise RuntimeError("rs.py runs the HIP generator and needs a GPU")
+        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(device)
+        return run_video(kw, device)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -99,4 +134,6 @@ if __name__ == "__main__":
     p.add_argument("--add_rate", type=float, default=0.2)
     p.add_argument("--mean", type=float, nargs=3, default=(0.485, 0.456, 0.406))
     p.add_argument("--std", type=float, nargs=3, default=(0.229, 0.224, 0.225))
+    p.add_argument("--video_size", type=str, default=None, help="WxH of a raw rgb24 video input")
+    p.add_argument("--fps", type=float, default=None, help="frame rate of a raw rgb24 video input")
     runer(**vars(p.parse_args()))
