@@ -83,6 +83,15 @@ class IsrBnDesc(ctypes.Structure):
                 ("dgamma", c_void_p), ("dbeta", c_void_p), ("gscale", c_float)]
 
 
+class IsrAdamArgs(ctypes.Structure):
+    _fields_ = [("step", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float),
+                ("weight_decay", c_float), ("bc2_sqrt", c_float)]
+
+
+MT_TENSOR_BYTES = 40  # isr_mt_tensor: 4 pointers + int64
+MT_CHUNK_BYTES = 16   # isr_mt_chunk: int32 t, int32 len, int64 start
+
+
 # Every symbol include/isr.h declares, with its ctypes signature.
 SIGNATURES = {
     "isr_conv3x3_packed_bytes": (c_size_t, [c_int32, c_int32]),
@@ -110,6 +119,11 @@ SIGNATURES = {
     "isr_conv3x3_fwd_variant": (c_int32, [POINTER(IsrConvDesc), c_int32, c_void_p]),
     "isr_head9x9_fwd": (c_int32, [POINTER(IsrHeadDesc), c_void_p]),
     "isr_tail9x9_fwd": (c_int32, [POINTER(IsrTailDesc), c_void_p]),
+    "isr_mt_adam": (c_int32, [c_void_p, c_void_p, c_int32, POINTER(IsrAdamArgs), c_void_p, c_void_p]),
+    "isr_mt_sumsq": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "isr_clip_coef": (c_int32, [c_void_p, c_int32, c_float, c_void_p, c_void_p]),
+    "isr_mt_scale": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "isr_mt_lerp": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p]),
     "isr_last_error": (ctypes.c_char_p, []),
     "isr_version": (c_int32, []),
 }

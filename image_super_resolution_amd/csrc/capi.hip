@@ -28,6 +28,12 @@ size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
 size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
 int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
 int wgrad3x3_dispatch(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
+int mt_adam_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, const isr_adam_args* a,
+                     const float* scale, hipStream_t s);
+int mt_sumsq_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, float* partial, hipStream_t s);
+int clip_coef_dispatch(const float* partial, int n, float max_norm, float* out, hipStream_t s);
+int mt_axpby_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, int mode, const float* coef, float d,
+                      hipStream_t s);
 }  // namespace isr
 
 static thread_local char g_err[512] = "";
@@ -74,6 +80,43 @@ static bool view_ok(const isr_view& v, int ha, int wa, int halo, int ch, const c
 extern "C" {
 
 const char* isr_last_error(void) { return g_err; }
+
+static int mt_ok(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, const char* what) {
+    if (!ts || !cs) return fail(ISR_ERR_BAD_DESC, "%s: null tensor / chunk table", what);
+    if (n <= 0 || n > (1 << 30)) return fail(ISR_ERR_BAD_DESC, "%s: bad chunk count %d", what, n);
+    return ISR_OK;
+}
+
+int isr_mt_adam(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, const isr_adam_args* a,
+                const float* scale, isr_stream_t s) {
+    if (int rc = mt_ok(ts, cs, n, "mt_adam")) return rc;
+    if (!a) return fail(ISR_ERR_BAD_DESC, "mt_adam: null args");
+    if (!(a->bc2_sqrt > 0.f) || !(a->beta1 >= 0.f && a->beta1 < 1.f) || !(a->beta2 >= 0.f && a->beta2 < 1.f))
+        return fail(ISR_ERR_BAD_DESC, "mt_adam: bad betas / bias correction");
+    return launched(isr::mt_adam_dispatch(ts, cs, n, a, scale, (hipStream_t)s), "mt_adam");
+}
+
+int isr_mt_sumsq(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, float* partial, isr_stream_t s) {
+    if (int rc = mt_ok(ts, cs, n, "mt_sumsq")) return rc;
+    if (!partial) return fail(ISR_ERR_BAD_DESC, "mt_sumsq: null partial buffer");
+    return launched(isr::mt_sumsq_dispatch(ts, cs, n, partial, (hipStream_t)s), "mt_sumsq");
+}
+
+int isr_clip_coef(const float* partial, int32_t n, float max_norm, float* out, isr_stream_t s) {
+    if (!partial || !out || n <= 0) return fail(ISR_ERR_BAD_DESC, "clip_coef: bad arguments");
+    return launched(isr::clip_coef_dispatch(partial, n, max_norm, out, (hipStream_t)s), "clip_coef");
+}
+
+int isr_mt_scale(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, const float* coef, isr_stream_t s) {
+    if (int rc = mt_ok(ts, cs, n, "mt_scale")) return rc;
+    if (!coef) return fail(ISR_ERR_BAD_DESC, "mt_scale: null coefficient");
+    return launched(isr::mt_axpby_dispatch(ts, cs, n, 0, coef, 0.f, (hipStream_t)s), "mt_scale");
+}
+
+int isr_mt_lerp(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, float d, isr_stream_t s) {
+    if (int rc = mt_ok(ts, cs, n, "mt_lerp")) return rc;
+    return launched(isr::mt_axpby_dispatch(ts, cs, n, 1, nullptr, d, (hipStream_t)s), "mt_lerp");
+}
 int isr_version(void) { return 1; }
 
 size_t isr_conv3x3_packed_bytes(int32_t cout, int32_t cin) { return isr::conv3x3_packed_bytes(cout, cin); }

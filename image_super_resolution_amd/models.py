@@ -374,8 +374,12 @@ class ModelEMA:
         ema_f = [v for v in self.ema.state_dict().values() if v.dtype.is_floating_point]
         src_f = [msd[k].detach() for k, v in self.ema.state_dict().items() if v.dtype.is_floating_point]
         # one multi-tensor lerp instead of the reference's per-tensor loop: v = v*d + (1-d)*m
-        torch._foreach_mul_(ema_f, d)
-        torch._foreach_add_(ema_f, src_f, alpha=1 - d)
+        if ema_f and ema_f[0].is_cuda:
+            from .optim import ema_update_
+            ema_update_(ema_f, src_f, d)  # HIP multi-tensor kernel (isr_mt_lerp)
+        else:
+            torch._foreach_mul_(ema_f, d)
+            torch._foreach_add_(ema_f, src_f, alpha=1 - d)
 
 
 def sliding_window(image: torch.Tensor, step, windowSize=None):

@@ -12,6 +12,8 @@ Differences, all deliberate:
   the GradScaler objects are kept for checkpoint compatibility.
 * the discriminator (stock PyTorch-ROCm ops) runs under bf16
   autocast where the reference uses fp16 autocast (train.py:91, :114).
+* Adam (optim.FusedAdam, built by train.py), clip_grad_norm_ and the EMA update
+  run as one HIP multi-tensor launch each (optim.py) instead of per-tensor loops.
 * loss.item() host syncs happen once per `log_every` iterations instead of
   every iteration (train.py:64-65, :101-112).
 * multi-GPU (one process per GPU): the generator's gradients are averaged by
@@ -24,9 +26,8 @@ from __future__ import annotations
 import time
 
 import torch
-from torch.nn.utils import clip_grad_norm_
-
 from .models import ModelEMA
+from .optim import clip_grad_norm_  # HIP multi-tensor clip (same signature as torch's)
 from .train_engine import allreduce_grads
 
 

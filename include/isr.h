@@ -271,6 +271,47 @@ int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_
 int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s);
 int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);
 
+/* ---- multi-tensor optimiser ops (one launch over every parameter) ---------
+ * A tensor is n fp32 elements at each non-null pointer (same element order);
+ * a chunk is elements [start, start + len) of tensor t.  The host builds the
+ * tensor and chunk tables in device memory (len <= 65536 recommended).
+ * Replaces: torch.optim.Adam.step (train.py:264-267, stepped at :58/:102/:118),
+ * clip_grad_norm_(params, 10) (train.py:57, :101, :116), ModelEMA.update
+ * (utils/models.py:31-40). */
+typedef struct isr_mt_tensor {
+    float* p; /* param (Adam), EMA tensor (lerp) */
+    float* g; /* grad (Adam, sumsq, scale), model tensor (lerp) */
+    float* m; /* exp_avg */
+    float* v; /* exp_avg_sq */
+    int64_t n;
+} isr_mt_tensor;
+
+typedef struct isr_mt_chunk {
+    int32_t t, len;
+    int64_t start;
+} isr_mt_chunk;
+
+/* torch.optim.Adam (amsgrad=False, maximize=False): g' = g*scale (+ wd*p);
+ * m = lerp(m, g', 1-beta1); v = beta2*v + (1-beta2)*g'^2;
+ * p += step * m / (sqrt(v)/bc2_sqrt + eps), step = -lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t). */
+typedef struct isr_adam_args {
+    float step, beta1, beta2, eps, weight_decay, bc2_sqrt;
+} isr_adam_args;
+
+/* `scale` (device, nullable): gradient multiplier applied on the fly (e.g. a clip coefficient). */
+int isr_mt_adam(const isr_mt_tensor* tensors, const isr_mt_chunk* chunks, int32_t nchunks, const isr_adam_args* a,
+                const float* scale, isr_stream_t s);
+/* partial[k] = sum of g^2 over chunk k. */
+int isr_mt_sumsq(const isr_mt_tensor* tensors, const isr_mt_chunk* chunks, int32_t nchunks, float* partial,
+                 isr_stream_t s);
+/* out[0] = sqrt(sum partial), out[1] = min(1, max_norm / (out[0] + 1e-6)) — clip_grad_norm_'s coefficient. */
+int isr_clip_coef(const float* partial, int32_t n, float max_norm, float* out, isr_stream_t s);
+/* g *= *coef over every chunk (clip_grad_norm_'s in-place scaling). */
+int isr_mt_scale(const isr_mt_tensor* tensors, const isr_mt_chunk* chunks, int32_t nchunks, const float* coef,
+                 isr_stream_t s);
+/* p = p*d + (1-d)*g over every chunk (ModelEMA.update: p = EMA tensor, g = model tensor). */
+int isr_mt_lerp(const isr_mt_tensor* tensors, const isr_mt_chunk* chunks, int32_t nchunks, float d, isr_stream_t s);
+
 const char* isr_last_error(void);
 int isr_version(void);
 
