@@ -30,33 +30,73 @@ def _dense(t: torch.Tensor) -> bool:
     return t.is_contiguous() or t.is_contiguous(memory_format=torch.channels_last)
 
 
+class _Uploader:
+    """Host → device upload of small int64 tables without a host sync: a ring of
+    pinned staging slots copied with non_blocking=True into a ring of device
+    slots (a pageable copy would block the host until the stream drains).  A
+    slot is reused `slots` uploads later, after its copy event has completed."""
+
+    def __init__(self, device, slots: int = 16, cap: int = 1 << 16):
+        self.device, self.cap = device, cap
+        self.host = [torch.empty(cap, dtype=torch.int64).pin_memory() for _ in range(slots)]
+        self.dev = [torch.empty(cap, dtype=torch.int64, device=device) for _ in range(slots)]
+        self.ev = [None] * slots
+        self.i = 0
+
+    def put(self, values: list[int]) -> torch.Tensor:
+        n = len(values)
+        if n > self.cap:
+            return torch.tensor(values, dtype=torch.int64).to(self.device)
+        k = self.i
+        self.i = (self.i + 1) % len(self.host)
+        if self.ev[k] is not None:
+            self.ev[k].synchronize()
+        self.host[k][:n] = torch.tensor(values, dtype=torch.int64)
+        d = self.dev[k][:n]
+        d.copy_(self.host[k][:n], non_blocking=True)
+        e = torch.cuda.Event()
+        e.record()
+        self.ev[k] = e
+        return d
+
+
+_UPLOADERS: dict = {}
+
+
+def _uploader(device) -> _Uploader:
+    key = str(device)
+    if key not in _UPLOADERS:
+        _UPLOADERS[key] = _Uploader(device)
+    return _UPLOADERS[key]
+
+
 class _Tables:
-    """Device copies of the isr_mt_tensor / isr_mt_chunk tables for one set of
-    pointers (cached: parameters and optimiser state do not move)."""
+    """isr_mt_tensor / isr_mt_chunk tables in device memory.  The chunk table
+    depends only on the tensor sizes (cached); the pointer table is uploaded
+    through the pinned ring whenever the pointers change (grads are new tensors
+    every step under zero_grad(set_to_none=True))."""
 
-    def __init__(self, rows: list[tuple[int, int, int, int, int]], device):
-        chunks = []
-        for ti, (*_, n) in enumerate(rows):
-            for s in range(0, n, CHUNK):
-                ln = min(CHUNK, n - s)
-                chunks.append((ti | (ln << 32), s))
-        self.n = len(chunks)
-        self.tensors = torch.tensor(rows, dtype=torch.int64).to(device)
-        self.chunks = torch.tensor(chunks, dtype=torch.int64).to(device) if chunks else None
+    def __init__(self):
+        self.chunks: dict[tuple, tuple[torch.Tensor, int]] = {}
+        self.ptrs: dict[tuple, torch.Tensor] = {}
 
-
-class _TableCache:
-    def __init__(self, cap: int = 8):
-        self.cap, self.d = cap, {}
-
-    def get(self, rows, device) -> _Tables:
+    def get(self, rows: list[tuple[int, int, int, int, int]], device) -> tuple[torch.Tensor, torch.Tensor, int]:
+        sizes = tuple(r[4] for r in rows)
+        ch = self.chunks.get(sizes)
+        if ch is None:
+            flat = []
+            for ti, n in enumerate(sizes):
+                for s in range(0, n, CHUNK):
+                    flat += [ti | (min(CHUNK, n - s) << 32), s]
+            ch = self.chunks[sizes] = (torch.tensor(flat, dtype=torch.int64).to(device), len(flat) // 2)
         key = tuple(rows)
-        t = self.d.get(key)
-        if t is None:
-            if len(self.d) >= self.cap:
-                self.d.pop(next(iter(self.d)))
-            t = self.d[key] = _Tables(rows, device)
-        return t
+        pt = self.ptrs.get(key)
+        if pt is None:
+            pt = _uploader(device).put([v for r in rows for v in r])
+            if len(self.ptrs) >= 4:  # keep a few stable pointer sets (params / EMA) resident
+                self.ptrs.pop(next(iter(self.ptrs)))
+            self.ptrs[key] = pt = pt.clone()
+        return pt, ch[0], ch[1]
 
 
 def _check(t: torch.Tensor, what: str):
@@ -78,7 +118,7 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
                                       maximize=False, foreach=None, capturable=False, differentiable=False,
                                       fused=None))
-        self._cache = _TableCache()
+        self._cache = _Tables()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -106,18 +146,18 @@ class FusedAdam(torch.optim.Optimizer):
                 by_step.setdefault(float(st["step"]), []).append(
                     (p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel()))
             for t, rows in by_step.items():
-                tab = self._cache.get(rows, group["params"][0].device)
-                if tab.n == 0:
+                pt, ch, n = self._cache.get(rows, group["params"][0].device)
+                if n == 0:
                     continue
                 bc1 = 1.0 - b1 ** t
                 a = _lib.IsrAdamArgs(step=-group["lr"] / bc1, beta1=b1, beta2=b2, eps=group["eps"],
                                      weight_decay=group["weight_decay"], bc2_sqrt=math.sqrt(1.0 - b2 ** t))
-                _lib.check(lib.isr_mt_adam(tab.tensors.data_ptr(), tab.chunks.data_ptr(), tab.n, ctypes.byref(a),
+                _lib.check(lib.isr_mt_adam(pt.data_ptr(), ch.data_ptr(), n, ctypes.byref(a),
                                            None, ops._stream()), "isr_mt_adam")
         return loss
 
 
-_CLIP_CACHE = _TableCache()
+_CLIP_CACHE = _Tables()
 
 
 @torch.no_grad()
@@ -136,21 +176,19 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
     lib = _lib.load()
     dev = grads[0].device
     rows = [(0, g.data_ptr(), 0, 0, g.numel()) for g in grads]
-    tab = _CLIP_CACHE.get(rows, dev)
-    partial = torch.empty(tab.n, dtype=torch.float32, device=dev)
+    pt, ch, n = _CLIP_CACHE.get(rows, dev)
+    partial = torch.empty(n, dtype=torch.float32, device=dev)
     out = torch.empty(2, dtype=torch.float32, device=dev)
     s = ops._stream()
-    _lib.check(lib.isr_mt_sumsq(tab.tensors.data_ptr(), tab.chunks.data_ptr(), tab.n, partial.data_ptr(), s),
-               "isr_mt_sumsq")
-    _lib.check(lib.isr_clip_coef(partial.data_ptr(), tab.n, float(max_norm), out.data_ptr(), s), "isr_clip_coef")
-    _lib.check(lib.isr_mt_scale(tab.tensors.data_ptr(), tab.chunks.data_ptr(), tab.n, out[1:].data_ptr(), s),
-               "isr_mt_scale")
+    _lib.check(lib.isr_mt_sumsq(pt.data_ptr(), ch.data_ptr(), n, partial.data_ptr(), s), "isr_mt_sumsq")
+    _lib.check(lib.isr_clip_coef(partial.data_ptr(), n, float(max_norm), out.data_ptr(), s), "isr_clip_coef")
+    _lib.check(lib.isr_mt_scale(pt.data_ptr(), ch.data_ptr(), n, out[1:].data_ptr(), s), "isr_mt_scale")
     if error_if_nonfinite and not torch.isfinite(out[0]).item():
         raise RuntimeError("clip_grad_norm_: the total norm of gradients is non-finite")
     return out[0]
 
 
-_EMA_CACHE = _TableCache()
+_EMA_CACHE = _Tables()
 
 
 @torch.no_grad()
@@ -166,6 +204,5 @@ def ema_update_(ema: list[torch.Tensor], model: list[torch.Tensor], d: float) ->
                                          not v.is_contiguous() else torch.contiguous_format)
             keep.append(m)  # alive until the launch is enqueued (stream-ordered reuse after that)
         rows.append((v.data_ptr(), m.data_ptr(), 0, 0, v.numel()))
-    tab = _EMA_CACHE.get(rows, ema[0].device)
-    _lib.check(_lib.load().isr_mt_lerp(tab.tensors.data_ptr(), tab.chunks.data_ptr(), tab.n, float(d), ops._stream()),
-               "isr_mt_lerp")
+    pt, ch, n = _EMA_CACHE.get(rows, ema[0].device)
+    _lib.check(_lib.load().isr_mt_lerp(pt.data_ptr(), ch.data_ptr(), n, float(d), ops._stream()), "isr_mt_lerp")
