@@ -24,10 +24,10 @@ int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s);
 int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s);
 int blocked_to_nchw_dispatch(const isr_convert_desc* d, hipStream_t s);
 int maxpool2_dispatch(const isr_pool_desc* d, int backward, hipStream_t s);
-size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
+size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d, int variant);
 size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
 int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
-int wgrad3x3_dispatch(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
+int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s);
 int mt_adam_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, const isr_adam_args* a,
                      const float* scale, hipStream_t s);
 int mt_sumsq_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, float* partial, hipStream_t s);
@@ -252,17 +252,29 @@ static int wgrad_validate(const isr_wgrad_desc* d) {
 
 size_t isr_wgrad3x3_workspace_bytes(const isr_wgrad_desc* d) {
     if (wgrad_validate(d) != ISR_OK) return 0;
-    return isr::wgrad3x3_workspace_bytes(d);
+    return isr::wgrad3x3_workspace_bytes(d, 0);
 }
 
-int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
+int isr_wgrad3x3_variant(const isr_wgrad_desc* d, int32_t variant, void* workspace, size_t ws_bytes,
+                         isr_stream_t s) {
     int rc = wgrad_validate(d);
     if (rc != ISR_OK) return rc;
     if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null workspace");
-    rc = isr::wgrad3x3_dispatch(d, workspace, ws_bytes, (hipStream_t)s);
+    if (variant < 0 || variant > 4) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: no variant %d", variant);
+    rc = isr::wgrad3x3_dispatch(d, variant, workspace, ws_bytes, (hipStream_t)s);
     if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: workspace of %zu bytes is smaller than %zu", ws_bytes,
-                              isr::wgrad3x3_workspace_bytes(d));
+                              isr::wgrad3x3_workspace_bytes(d, variant));
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: variant %d needs ha %% stage rows == 0", variant);
     return launched(rc, "wgrad3x3");
+}
+
+int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
+    return isr_wgrad3x3_variant(d, 0, workspace, ws_bytes, s);
+}
+
+size_t isr_wgrad3x3_variant_workspace_bytes(const isr_wgrad_desc* d, int32_t variant) {
+    if (wgrad_validate(d) != ISR_OK || variant < 0 || variant > 4) return 0;
+    return isr::wgrad3x3_workspace_bytes(d, variant);
 }
 
 static int wgrad9_validate(const isr_wgrad9_desc* d) {

@@ -262,10 +262,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
     }
 }
 
-using WG22 = WG<2, 2, 2>;
-using WG12 = WG<1, 2, 2>;
-using WG21 = WG<2, 1, 2>;
-using WG11 = WG<1, 1, 2>;
+// Variants (isr_wgrad3x3_variant; tools/tune_wgrad.py).  TY = pixel rows per
+// stage: a longer stage gives each barrier more MFMAs and halves the X halo
+// overhead ((TY+2)/TY), at the price of LDS (2 blocks/CU need <= 80 KB).
+template <int TY>
+struct Fam {
+    using C22 = WG<2, 2, TY>;
+    using C12 = WG<1, 2, TY>;
+    using C21 = WG<2, 1, TY>;
+    using C11 = WG<1, 1, TY>;
+};
 
 static int wgrad_splits(const isr_wgrad_desc* d, int tiles, int pairs) {
     if (d->splits > 0) return d->splits < tiles ? d->splits : tiles;
@@ -281,6 +287,7 @@ static void wgrad_geometry(const isr_wgrad_desc* d, int* tiles, int* splits) {
 
 template <class C>
 static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s) {
+    if (d->ha % C::TY) return -2;
     WgradArgs a;
     a.d = *d;
     wgrad_geometry<C>(d, &a.tiles, &a.splits);
@@ -300,17 +307,32 @@ static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipS
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <class F>
-static auto wgrad_pick(const isr_wgrad_desc* d, F&& f) {
-    const bool co2 = d->cout % 64 == 0, ci2 = d->cin % 64 == 0;
-    if (co2 && ci2) return f(WG22());
-    if (ci2) return f(WG12());
-    if (co2) return f(WG21());
-    return f(WG11());
+template <class Fm, class F>
+static auto pick_in(const isr_wgrad_desc* d, bool co1, F&& f) {
+    const bool co2 = !co1 && d->cout % 64 == 0, ci2 = d->cin % 64 == 0;
+    if (co2 && ci2) return f(typename Fm::C22());
+    if (ci2) return f(typename Fm::C12());
+    if (co2) return f(typename Fm::C21());
+    return f(typename Fm::C11());
 }
 
-size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d) {
-    return wgrad_pick(d, [&](auto c) {
+template <class F>
+static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
+    switch (variant) {
+        case 1: return pick_in<Fam<2>>(d, false, f);  // round-1 production: 2-row stages
+        case 2: return pick_in<Fam<4>>(d, false, f);  // 4-row stages (C22: 92 KB LDS, 1 block/CU)
+        case 3: return pick_in<Fam<4>>(d, true, f);   // 4-row stages, 32-cout tiles (<= 75 KB)
+        case 4: return f(Fam<8>::C11());              // 8-row stages, 32x32 tiles
+        default:
+            // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles with
+            // 8-row stages, or 4-row stages when cin % 64 == 32 (96, 160): 11-19 % over variant 1
+            if (d->cin % 64 == 32) return f(Fam<4>::C11());
+            return f(Fam<8>::C11());
+    }
+}
+
+size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d, int variant) {
+    return wgrad_pick(d, variant, [&](auto c) {
         using C = decltype(c);
         int tiles, splits;
         wgrad_geometry<C>(d, &tiles, &splits);
@@ -318,8 +340,8 @@ size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d) {
     });
 }
 
-int wgrad3x3_dispatch(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s) {
-    return wgrad_pick(d, [&](auto c) { return launch_wgrad<decltype(c)>(d, ws, ws_bytes, s); });
+int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s) {
+    return wgrad_pick(d, variant, [&](auto c) { return launch_wgrad<decltype(c)>(d, ws, ws_bytes, s); });
 }
 
 }  // namespace isr

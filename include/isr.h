@@ -168,6 +168,10 @@ int isr_wgrad9x9(const isr_wgrad9_desc* d, void* workspace, size_t ws_bytes, isr
 
 size_t isr_wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
 int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
+/* Tuning: the same computation by an explicit kernel variant (0 = production;
+ * 1..4 = stage-geometry alternatives, see wgrad3x3.hip), with its own workspace size. */
+size_t isr_wgrad3x3_variant_workspace_bytes(const isr_wgrad_desc* d, int32_t variant);
+int isr_wgrad3x3_variant(const isr_wgrad_desc* d, int32_t variant, void* workspace, size_t ws_bytes, isr_stream_t s);
 
 /* Elementwise combine on channel-blocked views (backward glue):
  *   y = (a*sa + b*sb) * (m > 0 ? 1 : mslope)   over c channels; b, m optional;
