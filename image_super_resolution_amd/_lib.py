@@ -96,6 +96,7 @@ MT_CHUNK_BYTES = 16   # isr_mt_chunk: int32 t, int32 len, int64 start
 SIGNATURES = {
     "isr_conv3x3_packed_bytes": (c_size_t, [c_int32, c_int32]),
     "isr_pack_conv3x3": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "isr_pack_conv3x3_batch": (c_int32, [c_void_p, c_int32, c_void_p]),
     "isr_pack_conv3x3_dgrad": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_float, c_int32, c_void_p]),
     "isr_wgrad3x3_workspace_bytes": (c_size_t, [POINTER(IsrWgradDesc)]),
     "isr_wgrad3x3": (c_int32, [POINTER(IsrWgradDesc), c_void_p, c_size_t, c_void_p]),

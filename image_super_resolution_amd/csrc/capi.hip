@@ -19,6 +19,7 @@ size_t tail9x9_packed_bytes();
 int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale, int sub2, hipStream_t s);
+int conv3x3_pack_batch(const isr_pack_item* items, int n, hipStream_t s);
 int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s);
 int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s);
 int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s);
@@ -80,6 +81,11 @@ static bool view_ok(const isr_view& v, int ha, int wa, int halo, int ch, const c
 extern "C" {
 
 const char* isr_last_error(void) { return g_err; }
+
+int isr_pack_conv3x3_batch(const isr_pack_item* items, int32_t n, isr_stream_t s) {
+    if (!items || n <= 0 || n > 65535) return fail(ISR_ERR_BAD_DESC, "pack_conv3x3_batch: bad item table (n=%d)", n);
+    return launched(isr::conv3x3_pack_batch(items, n, (hipStream_t)s), "pack_conv3x3_batch");
+}
 
 static int mt_ok(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, const char* what) {
     if (!ts || !cs) return fail(ISR_ERR_BAD_DESC, "%s: null tensor / chunk table", what);

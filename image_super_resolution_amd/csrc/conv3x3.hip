@@ -471,10 +471,11 @@ int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) { return conv3x3
 // scale * W[co(ci')][n][8 - tap] (180° rotation), where with sub2 the input
 // channel ci' = s*(layer cout/4) + c stands for layer channel co = 4c + s
 // (PixelShuffle order, see isr_conv_desc.x_sub2).
-__global__ void pack3x3_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int pcout, int pcin,
-                               int transposed, int sub2, float scale) {
+__device__ __forceinline__ void pack3x3_range(const float* __restrict__ w, __bf16* __restrict__ out, int pcout,
+                                              int pcin, int transposed, int sub2, float scale, size_t first,
+                                              size_t stride) {
     const size_t total = (size_t)pcout * pcin * 9;
-    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    for (size_t idx = first; idx < total; idx += stride) {
         size_t rem = idx;
         const int e = rem % 8; rem /= 8;
         const int hpos = rem % 2; rem /= 2;
@@ -493,6 +494,26 @@ __global__ void pack3x3_kernel(const float* __restrict__ w, __bf16* __restrict__
         }
         out[idx] = (__bf16)(v * scale);
     }
+}
+
+__global__ void pack3x3_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int pcout, int pcin,
+                               int transposed, int sub2, float scale) {
+    pack3x3_range(w, out, pcout, pcin, transposed, sub2, scale, blockIdx.x * (size_t)blockDim.x + threadIdx.x,
+                  (size_t)gridDim.x * blockDim.x);
+}
+
+// Many packs in one launch (the training plan repacks every conv each step):
+// blockIdx.y = item, blockIdx.x strides over that item's elements.
+__global__ void pack3x3_batch_kernel(const isr_pack_item* __restrict__ items) {
+    const isr_pack_item it = items[blockIdx.y];
+    const int pcout = it.dgrad ? it.cin : it.cout, pcin = it.dgrad ? it.cout : it.cin;
+    pack3x3_range(it.w, (__bf16*)it.out, pcout, pcin, it.dgrad, it.sub2, it.dgrad ? it.scale : 1.f,
+                  blockIdx.x * (size_t)blockDim.x + threadIdx.x, (size_t)gridDim.x * blockDim.x);
+}
+
+int conv3x3_pack_batch(const isr_pack_item* items, int n, hipStream_t s) {
+    hipLaunchKernelGGL(pack3x3_batch_kernel, dim3(96, n), dim3(256), 0, s, items);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 size_t conv3x3_packed_bytes(int cout, int cin) { return (size_t)cout * cin * 9 * 2; }

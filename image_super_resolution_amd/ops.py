@@ -134,6 +134,30 @@ def pack_conv3x3_dgrad(w: torch.Tensor, scale: float = 1.0, sub2: bool = False,
     return out
 
 
+def pack_batch_table(items, device) -> tuple[torch.Tensor, int]:
+    """Device table of isr_pack_item for isr_pack_conv3x3_batch.  items: tuples
+    (w fp32 [cout,cin,3,3], out packed bf16, cout, cin, dgrad, sub2, scale); the
+    tensors must stay alive and in place (parameters, packed buffers)."""
+    import struct
+    raw = bytearray()
+    for w, out, cout, cin, dgrad, sub2, scale in items:
+        _require_gpu(w, "pack_conv3x3_batch")
+        if w.dtype != torch.float32 or not w.is_contiguous() or tuple(w.shape) != (cout, cin, 3, 3):
+            raise ValueError("pack_conv3x3_batch: weights must be contiguous fp32 [cout, cin, 3, 3]")
+        if cin % 16 or cout % 32 or (dgrad and (cin % 32 or cout % 16)):
+            raise ValueError(f"pack_conv3x3_batch: unsupported shape cout={cout} cin={cin}")
+        if out.dtype != torch.bfloat16 or out.numel() * 2 < _lib.load().isr_conv3x3_packed_bytes(cout, cin):
+            raise ValueError("pack_conv3x3_batch: bad output buffer")
+        raw += struct.pack("<QQiiiifi", w.data_ptr(), out.data_ptr(), cout, cin, int(dgrad), int(sub2), float(scale), 0)
+    table = torch.frombuffer(bytes(raw), dtype=torch.uint8).to(device)
+    return table, len(items)
+
+
+def pack_batch(table: tuple[torch.Tensor, int]) -> None:
+    t, n = table
+    check(_lib.load().isr_pack_conv3x3_batch(t.data_ptr(), n, _stream()), "isr_pack_conv3x3_batch")
+
+
 def pack_head9x9(w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _require_gpu(w, "pack_head9x9")
     lib = _lib.load()

@@ -166,9 +166,21 @@ class GeneratorTrainPlan:
         return list(self._params)
 
     def pack(self) -> None:
-        """Refresh the packed bf16 weights from the fp32 parameters (every step)."""
+        """Refresh the packed bf16 weights from the fp32 parameters (every step):
+        every 3x3 conv's forward and dgrad pack in ONE launch (isr_pack_conv3x3_batch),
+        the two 9x9 convs separately."""
+        if getattr(self, "_pack_items", None) is None:
+            for c in self.convs:  # first call: allocate the packed buffers
+                c.pack()
+            self._pack_items = ops.pack_batch_table(
+                [(c.w, c.fwd, c.cout, c.cin, False, False, 1.0) for c in self.convs if c.kind == "3x3"]
+                + [(c.w, c.bwd, c.cout, c.cin, True, c.sub2, c.dgrad_scale) for c in self.convs if c.kind == "3x3"],
+                self.device)
+            return
+        ops.pack_batch(self._pack_items)
         for c in self.convs:
-            c.pack()
+            if c.kind != "3x3":
+                c.pack()
 
     def _build(self):
         a, lib = self.a, self.lib

@@ -261,6 +261,17 @@ int isr_pack_conv3x3(const float* w_oihw, void* packed, int32_t cout, int32_t ci
  * (the Scaler backward, utils/models.py:583). */
 int isr_pack_conv3x3_dgrad(const float* w_oihw, void* packed, int32_t cout, int32_t cin, float scale, int32_t sub2,
                            isr_stream_t s);
+/* Many isr_pack_conv3x3 / isr_pack_conv3x3_dgrad in one launch (items: device array). */
+typedef struct isr_pack_item {
+    const float* w; /* layer weights [cout][cin][3][3] fp32 */
+    void* out;      /* packed bf16, isr_conv3x3_packed_bytes(cout, cin) bytes */
+    int32_t cout, cin;
+    int32_t dgrad;  /* 0: forward pack; 1: dgrad pack (as isr_pack_conv3x3_dgrad) */
+    int32_t sub2;
+    float scale;
+    int32_t pad_;
+} isr_pack_item;
+int isr_pack_conv3x3_batch(const isr_pack_item* items, int32_t n, isr_stream_t s);
 size_t isr_head9x9_packed_bytes(int32_t cout, int32_t cin);
 int isr_pack_head9x9(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
 size_t isr_tail9x9_packed_bytes(int32_t cout, int32_t cin);

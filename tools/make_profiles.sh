@@ -9,18 +9,19 @@
 set -eu
 R=${1:-r01}
 export TMPDIR=/tmp
-P=gpurun_out/profiles_$R   # gpurun merges only gpurun_out/ back; copy into profiles/ afterwards
-mkdir -p $P
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench_$R -o bench -- \
-  python3 bench.py --round $R > gpurun_out/prof_bench_$R.json 2> gpurun_out/prof_bench_$R.err
-cp gpurun_out/prof_bench_$R/bench_kernel_stats.csv $P/${R}_bench_kernel_stats.csv
-bash tools/profile_pmc.sh gpurun_out/pmc_bench_$R bench.py --no-cpu-baseline --steps 5 --warmup 2 --round $R
-python3 tools/pmc_summary.py gpurun_out/pmc_bench_$R --json $P/${R}_pmc_summary.json > /dev/null
+P=gpurun_out/profiles_$R   # gpurun merges only gpurun_out/ back (<= 64 MiB); copy into profiles/ afterwards
+T=/tmp/isr_prof_$R         # raw rocprofv3 output stays off gpurun_out/
+mkdir -p $P $T
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/prof_bench -o bench -- \
+  python3 bench.py --round $R > $P/prof_bench.json 2> $T/prof_bench.err
+cp $T/prof_bench/bench_kernel_stats.csv $P/${R}_bench_kernel_stats.csv
+bash tools/profile_pmc.sh $T/pmc_bench bench.py --no-cpu-baseline --steps 5 --warmup 2 --round $R
+python3 tools/pmc_summary.py $T/pmc_bench --json $P/${R}_pmc_summary.json > /dev/null
 python3 - "$R" "$P" <<'EOF'
 import json, sys
 R, P = sys.argv[1], sys.argv[2]
 rows = json.load(open(f"{P}/{R}_pmc_summary.json"))
-dom = [r for r in rows if "192, 0, 0>" in r["kernel"] or "192>" in r["kernel"]]  # RDB final conv (V_F0)
+dom = [r for r in rows if "conv3x3_fwd_kernel" in r["kernel"] and ", 192, " in r["kernel"]]  # RDB final conv (V_F0)
 if dom:
     r = dom[0]
     out = {"kernel": r["kernel"], "grid": r["grid"], "dispatches": r["dispatches"],
@@ -33,8 +34,8 @@ if dom:
     print("traffic", out["hbm_bytes_per_launch"])
 EOF
 cp $P/${R}_pmc_traffic.json profiles/ 2>/dev/null || true
-timeout -k 10 600 python3 bench.py --round $R > $P/${R}_bench.json 2> gpurun_out/bench_final_$R.err
+timeout -k 10 600 python3 bench.py --round $R > $P/${R}_bench.json 2> $T/bench_final.err
 cat $P/${R}_bench.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_train_$R -o train -- \
-  python3 tools/bench_train.py --steps 3 --warmup 2 > $P/${R}_train_bench.json 2> gpurun_out/prof_train_$R.err
-cp gpurun_out/prof_train_$R/train_kernel_stats.csv $P/${R}_train_kernel_stats.csv
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/prof_train -o train -- \
+  python3 tools/bench_train.py --steps 3 --warmup 2 > $P/${R}_train_bench.json 2> $T/prof_train.err
+cp $T/prof_train/train_kernel_stats.csv $P/${R}_train_kernel_stats.csv
