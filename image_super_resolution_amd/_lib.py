@@ -28,7 +28,8 @@ class IsrConvDesc(ctypes.Structure):
                 ("x", IsrView), ("y", IsrView), ("y2", IsrView), ("r1", IsrView), ("r2", IsrView),
                 ("wpack", c_void_p), ("bias", c_void_p),
                 ("slope", c_float), ("s1", c_float), ("s2", c_float), ("shuffle", c_int32),
-                ("m", IsrView), ("mslope", c_float), ("m_c0", c_int32), ("r1_cn", c_int32), ("x_sub2", c_int32)]
+                ("m", IsrView), ("mslope", c_float), ("m_c0", c_int32), ("r1_cn", c_int32), ("x_sub2", c_int32),
+                ("taps", c_int32)]
 
 
 class IsrHeadDesc(ctypes.Structure):

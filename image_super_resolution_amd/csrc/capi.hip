@@ -169,6 +169,8 @@ static int conv3x3_validate(const isr_conv_desc* d) {
         return fail(ISR_ERR_UNSUPPORTED, "conv3x3: cout %d must be a positive multiple of 32", d->cout);
     if (!d->wpack) return fail(ISR_ERR_BAD_DESC, "conv3x3: null weights");
     if (d->shuffle != 1 && d->shuffle != 2) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: shuffle must be 1 or 2");
+    if (d->taps < 0 || d->taps > 2) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: taps must be 0, 1 or 2");
+    if (d->taps && d->cout % 64) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: a 2x2 tap window needs cout %% 64 == 0");
     if (d->x_sub2) {
         if (d->cin % 128) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: x_sub2 needs cin %% 128 == 0 (got %d)", d->cin);
         if (d->shuffle != 1) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: x_sub2 with a shuffled store");

@@ -24,11 +24,19 @@
 
 namespace isr {
 
-template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1), int EPQ_ = 4>
+template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1), int EPQ_ = 4,
+          int SPL_ = 1, int TWN_ = 0>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
     static constexpr int PIPE = PIPE_; // 1: double-buffered fragment registers across (k-step, dx) steps
     static constexpr int EPQ = EPQ_;   // epilogue operand units (8 VGPRs each) loaded per pass
+    static constexpr int SPL = SPL_;   // the next chunk's LDS-DMA issued in SPL parts, one before each of the first SPL steps
+    // tap window: 0 = all 3x3 taps; 1 = taps {0,1}^2; 2 = taps {1,2}^2 (the 2x2 convs that a
+    // stride-2 3x3 conv and its transpose become on the 2x2 phase decomposition, isr_conv_desc.taps)
+    static constexpr int TWN = TWN_;
+    static constexpr int TLO = TWN == 2 ? 1 : 0;
+    static constexpr int TN = TWN ? 2 : 3;
+    static constexpr int NA = R + TN - 1;  // input rows one wave reads per step
     static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol)
     // Ablation bits, timing-only builds (outputs wrong): 1 = no MFMA (operands
     // kept live), 2 = stage only chunk 0 (no refill), 4 = no epilogue stores.
@@ -263,12 +271,12 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         off[k] = o;
     }
 
-    auto stage = [&](int chunk, int buf) {
+    auto stage = [&](int chunk, int buf, int k0 = 0, int k1 = C::IPW) {
         char* dst = smem + buf * C::STAGE;
         const char* xs = xbase + xchunk(chunk);
         const char* ws = wbase + (size_t)chunk * wchunk_bytes;
 #pragma unroll
-        for (int k = 0; k < C::IPW; ++k) {
+        for (int k = k0; k < k1; ++k) {
             const int j = wave + WM * k;
             const char* src = (j < C::HALO_INSTR ? xs : ws) + off[k];
             glds16(src, dst + j * 1024);
@@ -306,36 +314,46 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (!(C::ABL & 2) && chunk + C::NST - 1 < nchunks) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+        const bool refill = !(C::ABL & 2) && chunk + C::NST - 1 < nchunks;
+        if constexpr (C::SPL <= 1) {
+            if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+        }
 
         const char* hs = smem + ((C::ABL & 2) ? 0 : (chunk % C::NST)) * C::STAGE;
         const char* ws = hs + C::HALO_INSTR * 1024;
         // Software pipeline over the chunk's (k-step, dx) steps: the fragments of
         // step st+1 are read into the other register set while step st's MFMAs
         // run, so LDS latency is covered by MFMA work of the same wave.
-        constexpr int NS = C::KS * 3;
-        bf16x8 fb[2][3][NF], fa[2][R + 2];
+        constexpr int NS = C::KS * C::TN;
+        constexpr int TN = C::TN, TLO = C::TLO, NA = C::NA;
+        bf16x8 fb[2][TN][NF], fa[2][NA];
         auto load_step = [&](int st, int set) {
-            const int ks = st / 3, dx = st - 3 * (st / 3);
+            const int ks = st / TN, dx = TLO + st % TN;
             const char* hp = hs + ks * C::HIPL * 1024;
 #pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
+            for (int dyi = 0; dyi < TN; ++dyi)
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
                     const int n = f * 32 + l31;
-                    const int u = ((ks * 9 + dy * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
-                    fb[set][dy][f] = lds_read16(ws + u * 16);
+                    const int u = ((ks * 9 + (TLO + dyi) * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
+                    fb[set][dyi][f] = lds_read16(ws + u * 16);
                 }
 #pragma unroll
-            for (int i = 0; i < R + 2; ++i) {
-                const int q = qw + i * C::HC + dx;
-                fa[set][i] = lds_read16(hp + halo_unit2(q, hh) * 16);
+            for (int ia = 0; ia < NA; ++ia) {
+                const int q = qw + (TLO + ia) * C::HC + dx;
+                fa[set][ia] = lds_read16(hp + halo_unit2(q, hh) * 16);
             }
         };
         if constexpr (C::PIPE) load_step(0, 0);
 #pragma unroll
         for (int st = 0; st < NS; ++st) {
             const int cur = C::PIPE ? (st & 1) : 0;
+            if constexpr (C::SPL > 1) {
+                static_assert(C::SPL <= NS, "refill parts must fit the chunk's steps");
+                if (st < C::SPL && refill)
+                    stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST, st * C::IPW / C::SPL,
+                          (st + 1) * C::IPW / C::SPL);
+            }
             if constexpr (C::PIPE) {
                 if (st + 1 < NS) load_step(st + 1, cur ^ 1);
                 // keep the prefetch ahead of this step's MFMAs (hipcc otherwise sinks
@@ -344,18 +362,19 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
             } else {
                 load_step(st, 0);
             }
+            // input row TLO+ia feeds output row r through kernel row dy = TLO+dyi: r = ia - dyi
 #pragma unroll
-            for (int i = 0; i < R + 2; ++i) {
+            for (int ia = 0; ia < NA; ++ia) {
 #pragma unroll
-                for (int dy = 0; dy < 3; ++dy) {
-                    const int r = i - dy;
+                for (int dyi = 0; dyi < TN; ++dyi) {
+                    const int r = ia - dyi;
                     if (r >= 0 && r < R) {
 #pragma unroll
                         for (int f = 0; f < NF; ++f) {
                             if constexpr (C::ABL & 1) {
-                                asm volatile("" ::"v"(fa[cur][i]), "v"(fb[cur][dy][f]));
+                                asm volatile("" ::"v"(fa[cur][ia]), "v"(fb[cur][dyi][f]));
                             } else {
-                                acc[r][f] = mfma32(fb[cur][dy][f], fa[cur][i], acc[r][f]);
+                                acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
                             }
                         }
                     }
@@ -443,6 +462,8 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 6: return launch3x3<C3<4, 4, 1, 16, 2, 0, 4>>(d, s);
             case 7: return launch3x3<C3<4, 4, 1, 16, 2, 0, 3>>(d, s);
             case 8: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 1>>(d, s);  // V_G0, one unit per epilogue pass
+            case 9: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 4, 2>>(d, s);  // V_G0, refill split over 2 steps
+            case 10: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 4, 3>>(d, s); // V_G0, refill split over 3 steps
         }
         return -2;
     }
@@ -458,11 +479,21 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
         case 7: return launch3x3<C3<4, 4, 2, 16, 2, 0, 3>>(d, s);
         case 8: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 0, 1>>(d, s)  // V_F0 / V_W0, one unit per pass
                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 1>>(d, s);
+        case 9: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 0, 4, 2>>(d, s)  // refill split over 2 steps
+                                     : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 2>>(d, s);
+        case 10: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 1, 4, 1>>(d, s)  // pipelined fragment reads
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 1, 4, 1>>(d, s);
+        case 11: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 1, 4, 2>>(d, s)  // both
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 1, 4, 2>>(d, s);
     }
     return -2;
 }
 
-int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) { return conv3x3_fwd_variant(d, 0, s); }
+int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) {
+    if (d->taps == 1) return d->cout % 64 ? -2 : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 1, 1>>(d, s);
+    if (d->taps == 2) return d->cout % 64 ? -2 : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 1, 2>>(d, s);
+    return conv3x3_fwd_variant(d, 0, s);
+}
 
 // ---- weight packing: fp32 OIHW → bf16 [c16][tap][cout][hpos][8] -----------
 // Forward: the packed conv has (cout, cin) = the layer's, element W[n][ci][tap].

@@ -397,8 +397,12 @@ def sliding_window(image: torch.Tensor, step, windowSize=None):
 
 
 class Discriminator(nn.Module):
-    """SRGAN discriminator (utils/models.py:513-569).  Out of kernel scope
-    (SURVEY.md §2 row 7): runs on stock PyTorch-ROCm ops so SRGAN mode trains."""
+    """SRGAN discriminator (utils/models.py:513-569).  `use_libisr(True)` runs the
+    eight conv blocks in train mode (incl. the stride-2 ones and train-mode
+    BatchNorm) on libisr (discriminator.py); the adaptive pool and the two Linear
+    layers are torch ops either way.  Off by default: at [16,3,512,512] the libisr
+    stack (10.6 ms fwd+bwd, its stride-2 wgrad still computes all 9 phase taps) is
+    slower than MIOpen in NHWC with find mode (8.9 ms, tools/bench_disc.py)."""
 
     def __init__(self, kernel_size=3, n_channels=64, n_blocks=8, fc_size=1024):
         super().__init__()
@@ -418,9 +422,18 @@ class Discriminator(nn.Module):
         self.fc1 = nn.Sequential(nn.Linear(out_channels * 6 ** 2, fc_size), nn.LeakyReLU(0.2))
         self.fc2 = nn.Linear(fc_size, 1)
 
+    def use_libisr(self, enable: bool = True) -> "Discriminator":
+        self.__dict__["hip"] = bool(enable)
+        return self
+
     def forward(self, inputs):
         b = inputs.size(0)
-        out = self.adaptive_pool(self.conv_blocks(inputs))
+        if self.training and inputs.is_cuda and self.__dict__.get("hip", False):
+            from .discriminator import conv_stack_train
+            feat = conv_stack_train(self, inputs)
+        else:
+            feat = self.conv_blocks(inputs)
+        out = self.adaptive_pool(feat)
         return self.fc2(self.fc1(out.reshape(b, -1)))
 
 

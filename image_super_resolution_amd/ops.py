@@ -48,12 +48,15 @@ class ActBuffer:
 
     @staticmethod
     def alloc(n: int, h: int, w: int, c: int, pad: int, device, ha: int | None = None,
-              wa: int | None = None) -> "ActBuffer":
+              wa: int | None = None, min_hp: int = 0, min_wp: int = 0) -> "ActBuffer":
+        """min_hp / min_wp: extra zero rows / columns below / right of the computed
+        region (a stride-2 consumer reads 2*ha_out + 2*pad rows of its input)."""
         if c % 16:
             raise ValueError(f"ActBuffer channels must be a multiple of 16, got {c}")
         ha = round_up(h, TILE_H) if ha is None else ha
         wa = round_up(w, TILE_W) if wa is None else wa
-        t = torch.zeros((n, c // 16, ha + 2 * pad, wa + 2 * pad, 16), dtype=torch.bfloat16, device=device)
+        hp, wp = max(ha + 2 * pad, min_hp), max(wa + 2 * pad, min_wp)
+        t = torch.zeros((n, c // 16, hp, wp, 16), dtype=torch.bfloat16, device=device)
         return ActBuffer(t, n, h, w, ha, wa, pad)
 
     @property
@@ -193,12 +196,13 @@ def conv3x3_desc(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor
                  r2: ActBuffer | None = None, r2_coff: int = 0, s2: float = 1.0,
                  y2: ActBuffer | None = None, y2_coff: int = 0, shuffle: int = 1,
                  m: ActBuffer | None = None, m_coff: int | None = None, mslope: float = 1.0, m_c0: int = 0,
-                 r1_cn: int = 0, x_sub2: bool = False) -> IsrConvDesc:
+                 r1_cn: int = 0, x_sub2: bool = False, taps: int = 0) -> IsrConvDesc:
     """Descriptor for y[..., y_coff:y_coff+cout] = epilogue(conv3x3(x[..., x_coff:x_coff+cin])).
 
     Backward extensions: `m` (read at channel m_coff, default y_coff) masks output
     channels >= m_c0 with LeakyReLU'(m) of slope `mslope`; `r1_cn` limits r1 to the
-    first r1_cn output channels; `x_sub2` reads x (2h x 2w grid) as PixelShuffle(2)ᵀ."""
+    first r1_cn output channels; `x_sub2` reads x (2h x 2w grid) as PixelShuffle(2)ᵀ;
+    `taps` 1 / 2 restricts the conv to kernel taps {0,1}² / {1,2}² (stride-2 convs, see isr.h)."""
     d = IsrConvDesc()
     d.n, d.h, d.w, d.ha, d.wa = x.n, x.h, x.w, x.ha, x.wa
     d.cin, d.cout = cin, cout
@@ -214,6 +218,7 @@ def conv3x3_desc(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor
         d.n, d.h, d.w, d.ha, d.wa = y.n, y.h, y.w, y.ha, y.wa
     d.m = m.view(y_coff if m_coff is None else m_coff) if m is not None else _NULL_VIEW
     d.mslope, d.m_c0, d.r1_cn, d.x_sub2 = mslope, m_c0, r1_cn, int(bool(x_sub2))
+    d.taps = taps
     return d
 
 

@@ -85,6 +85,10 @@ typedef struct isr_conv_desc {
     int32_t x_sub2;    /* 1: input channel c' = s*(cin/4) + c reads x at pixel (2y + (s>>1), 2x + (s&1)),
                           channel c (x is on the 2h x 2w grid, pad >= 2): the transpose of
                           PixelShuffle(2) (utils/models.py:583) folded into the load; cin % 128 == 0 */
+    int32_t taps;      /* 0: all 3x3 taps; 1: only taps {0,1}^2; 2: only taps {1,2}^2 (cout % 64 == 0).
+                          A stride-2 3x3 conv (Discriminator, utils/models.py:533-542) is taps=1 over the
+                          x_sub2 view with 4*cin phase-expanded weights; its input gradient is taps=2
+                          over the output gradient with shuffle == 2 (4*cin phase outputs). */
 } isr_conv_desc;
 
 /* 9x9 head conv, 3 → cout (=64) channels, input NCHW (fp32 already normalised,

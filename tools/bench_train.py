@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--mode", default="srgan", choices=["srgan", "pixel"])
     ap.add_argument("--dis-layout", default="nhwc", choices=["nchw", "nhwc"],
                     help="discriminator memory format (stock MIOpen convs)")
+    ap.add_argument("--dis-libisr", action="store_true", help="discriminator conv stack on libisr")
     ap.add_argument("--no-miopen-find", dest="miopen_find", action="store_false",
                     help="torch.backends.cudnn.benchmark = False (default: MIOpen find mode on, as train.py)")
     args = ap.parse_args()
@@ -53,6 +54,7 @@ def main():
     if args.mode == "srgan":
         gen = models.SRGAN(args.blocks, 0.2, True, 4).to(dev)
         dis = models.Discriminator(3, 64, 8, 1024).to(dev)
+        dis.use_libisr(args.dis_libisr)
         if args.dis_layout == "nhwc":
             dis = dis.to(memory_format=torch.channels_last)
         torch.backends.cudnn.benchmark = args.miopen_find

@@ -138,7 +138,7 @@ def main(opt):
     else:
         gen_net = models.SRGAN(opt.rs_deep, opt.add_rate, opt.enchant, opt.scale)
         gen_net.init_weight(pretrained=res_ck.as_posix())
-        dis_net = models.Discriminator(3, 64, 8, 1024)
+        dis_net = models.Discriminator(3, 64, 8, 1024).use_libisr(opt.dis_libisr)
         ema = models.ModelEMA(gen_net, tau=opt.epochs * iters)
         optimizer_g = optim.FusedAdam(gen_net.parameters(), lr=opt.lr, betas=(0.9, 0.999),
                                        weight_decay=opt.weight_decay)
@@ -222,6 +222,8 @@ def parse(argv=None):
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--steps", type=int, default=0, help="iterations per epoch (0 = one pass over the data)")
     p.add_argument("--vgg_weights", type=str, default=None)
+    p.add_argument("--dis_libisr", action="store_true", help="run the discriminator's conv stack on libisr "
+                   "(default: MIOpen NHWC, currently faster; DESIGN.md §8)")
     opt = p.parse_args(argv)
     if not opt.data and Path("train_images.json").is_file():
         opt.data = "train_images.json"
