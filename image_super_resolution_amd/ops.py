@@ -152,7 +152,7 @@ def pack_batch_table(items, device) -> tuple[torch.Tensor, int]:
         if out.dtype != torch.bfloat16 or out.numel() * 2 < _lib.load().isr_conv3x3_packed_bytes(cout, cin):
             raise ValueError("pack_conv3x3_batch: bad output buffer")
         raw += struct.pack("<QQiiiifi", w.data_ptr(), out.data_ptr(), cout, cin, int(dgrad), int(sub2), float(scale), 0)
-    table = torch.frombuffer(bytes(raw), dtype=torch.uint8).to(device)
+    table = torch.frombuffer(raw, dtype=torch.uint8).to(device)
     return table, len(items)
 
 

@@ -27,7 +27,10 @@ def step(m, need_dx):
     o.float().sum().backward()
 
 
-for name, m in (("libisr", hip), ("miopen_nhwc_amp", stock)):
+impls = (("libisr", hip), ("miopen_nhwc_amp", stock))
+if len(sys.argv) > 1:
+    impls = [i for i in impls if i[0] == sys.argv[1]]
+for name, m in impls:
     for need_dx in (False, True):
         for _ in range(3):
             step(m, need_dx)
