@@ -464,6 +464,9 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 8: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 1>>(d, s);  // V_G0, one unit per epilogue pass
             case 9: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 4, 2>>(d, s);  // V_G0, refill split over 2 steps
             case 10: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 4, 3>>(d, s); // V_G0, refill split over 3 steps
+            case 11: return launch3x3<C3<2, 4, 1, 16, 3>>(d, s);  // 8x32 tile, 3-deep ring (60 KB, 2 blocks/CU)
+            case 12: return launch3x3<C3<4, 4, 1, 16, 3>>(d, s);  // 16x32 tile, 3-deep ring (1 block/CU)
+            case 13: return launch3x3<C3<2, 4, 1, 16, 2>>(d, s);  // 8x32 tile, double buffer (3 blocks/CU)
         }
         return -2;
     }
