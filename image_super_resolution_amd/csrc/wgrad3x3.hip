@@ -39,10 +39,13 @@ __device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int NCO_, int NCI_, int TY_>
+template <int NCO_, int NCI_, int TY_, int KW_ = 1>
 struct WG {
     static constexpr int NCO = NCO_, NCI = NCI_, TY = TY_;
-    static constexpr int WM = 3, NT = 64 * WM;
+    // KW waves per kernel row dy split each stage's K (pixel groups) between them;
+    // their partial sums are added through LDS before the workspace store
+    static constexpr int KW = KW_;
+    static constexpr int WM = 3 * KW, NT = 64 * WM;
     static constexpr int CO_T = 32 * NCO, CI_T = 32 * NCI;
     static constexpr int GPL = 2 * NCO, XPL = 2 * NCI;         // 16-channel planes per stage
     static constexpr int XPIX = (TY + 2) * 34;                  // halo pixels per plane
@@ -56,8 +59,10 @@ struct WG {
     static constexpr int STAGE = G_BYTES + XPL * X_PLANE;
     static constexpr int G_INSTR = GPL * G_IPL, INSTR = G_INSTR + XPL * X_IPL;
     static constexpr int IPW = (INSTR + WM - 1) / WM;
-    static constexpr int LDS = 2 * STAGE;
+    static constexpr int RED = (KW - 1) * 3 * 64 * (3 * NCO * NCI * 16 + NCO) * 4;  // cross-wave K reduction
+    static constexpr int LDS = 2 * STAGE > RED ? 2 * STAGE : RED;
     static_assert(LDS <= 163840, "LDS budget");
+    static_assert((2 * TY) % KW == 0, "K groups split evenly between the KW waves of a row");
 };
 
 struct WgradArgs {
@@ -77,7 +82,8 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
     const int cot = b % ncot; b /= ncot;
     const int split = b;
     const int t0 = (int)((long)split * a.tiles / a.splits), t1 = (int)((long)(split + 1) * a.tiles / a.splits);
-    const int wave = wave_id();  // = dy
+    const int wave = wave_id();
+    const int dy = wave % 3, kh = wave / 3;  // kernel row, K-share of this wave
     const int lane = threadIdx.x & 63;
     const int nbx = d.wa / 32, nby = d.ha / TY;
 
@@ -148,7 +154,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
     float bsum[NCO];
 #pragma unroll
     for (int f = 0; f < NCO; ++f) bsum[f] = 0.f;
-    const bool do_bias = d.db && cit == 0 && wave == 1;
+    const bool do_bias = d.db && cit == 0 && dy == 1;
 
     // transposed-read lane geometry: plane gi of the 32-channel fragment, pixel q + 8h, channels 4p..4p+3
     const int gi = (lane >> 4) & 1, hh = lane >> 5, q = (lane >> 2) & 3, p = lane & 3;
@@ -164,7 +170,8 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         if (t + 1 < t1) stage(t + 1, cur ^ 1);
         const char* base = smem + cur * C::STAGE;
 #pragma unroll
-        for (int kg = 0; kg < 2 * TY; ++kg) {
+        for (int kk = 0; kk < 2 * TY / C::KW; ++kk) {
+            const int kg = kk * C::KW + kh;
             const int r = kg >> 1, c0 = (kg & 1) * 16;
             bf16x8 fa[NCO];
 #pragma unroll
@@ -183,7 +190,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
                 bf16x8 fb[NCI];
 #pragma unroll
                 for (int e = 0; e < NCI; ++e) {
-                    const char* pb = base + b_lane + 2 * e * C::X_PLANE + ((r + wave) * 34 + c0 + dx) * 32;
+                    const char* pb = base + b_lane + 2 * e * C::X_PLANE + ((r + dy) * 34 + c0 + dx) * 32;
                     fb[e] = cat4(lds_tr4(pb), lds_tr4(pb + 4 * 32));
                 }
 #pragma unroll
@@ -194,12 +201,51 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         }
     }
 
+    if constexpr (C::KW > 1) {
+        // add the K-shares of the KW waves of each kernel row (through the now idle stage LDS)
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        constexpr int PER = 3 * NCO * NCI * 16 + NCO;  // floats per lane
+        float* red = reinterpret_cast<float*>(smem);
+        if (kh > 0) {
+            float* dst = red + ((size_t)((kh - 1) * 3 + dy) * 64 + lane) * PER;
+            int q = 0;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int f = 0; f < NCO; ++f)
+#pragma unroll
+                    for (int e = 0; e < NCI; ++e)
+#pragma unroll
+                        for (int g = 0; g < 16; ++g) dst[q++] = acc[dx][f][e][g];
+#pragma unroll
+            for (int f = 0; f < NCO; ++f) dst[q++] = bsum[f];
+        }
+        __syncthreads();
+        if (kh > 0) return;
+#pragma unroll
+        for (int k = 1; k < C::KW; ++k) {
+            const float* src = red + ((size_t)((k - 1) * 3 + dy) * 64 + lane) * PER;
+            int q = 0;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                for (int f = 0; f < NCO; ++f)
+#pragma unroll
+                    for (int e = 0; e < NCI; ++e)
+#pragma unroll
+                        for (int g = 0; g < 16; ++g) acc[dx][f][e][g] += src[q++];
+#pragma unroll
+            for (int f = 0; f < NCO; ++f) bsum[f] += src[q++];
+        }
+    }
+
     // ---- partial sums: ws[split][tap][co][ci], D[co = (g&3)+8(g>>2)+4h][ci = l31]
     const int l31 = lane & 31;
     float* wsp = a.ws + (size_t)split * (9 * d.cout * d.cin + d.cout);
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
-        float* wt = wsp + (size_t)(wave * 3 + dx) * d.cout * d.cin;
+        float* wt = wsp + (size_t)(dy * 3 + dx) * d.cout * d.cin;
 #pragma unroll
         for (int f = 0; f < NCO; ++f)
 #pragma unroll
@@ -211,7 +257,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
                     wt[(size_t)co * d.cin + ci] = acc[dx][f][e][g];
                 }
     }
-    if (d.db && cit == 0 && wave == 1) {
+    if (d.db && cit == 0 && dy == 1) {
         float* bp = wsp + (size_t)9 * d.cout * d.cin;
 #pragma unroll
         for (int f = 0; f < NCO; ++f) {
@@ -265,12 +311,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
 // Variants (isr_wgrad3x3_variant; tools/tune_wgrad.py).  TY = pixel rows per
 // stage: a longer stage gives each barrier more MFMAs and halves the X halo
 // overhead ((TY+2)/TY), at the price of LDS (2 blocks/CU need <= 80 KB).
-template <int TY>
+template <int TY, int KW = 1>
 struct Fam {
-    using C22 = WG<2, 2, TY>;
-    using C12 = WG<1, 2, TY>;
-    using C21 = WG<2, 1, TY>;
-    using C11 = WG<1, 1, TY>;
+    using C22 = WG<2, 2, TY, KW>;
+    using C12 = WG<1, 2, TY, KW>;
+    using C21 = WG<2, 1, TY, KW>;
+    using C11 = WG<1, 1, TY, KW>;
 };
 
 static int wgrad_splits(const isr_wgrad_desc* d, int tiles, int pairs) {
@@ -287,7 +333,7 @@ static void wgrad_geometry(const isr_wgrad_desc* d, int* tiles, int* splits) {
 
 template <class C>
 static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s) {
-    if (d->ha % C::TY) return -2;
+    if (d->ha % C::TY || d->cout % C::CO_T || d->cin % C::CI_T) return -2;
     WgradArgs a;
     a.d = *d;
     wgrad_geometry<C>(d, &a.tiles, &a.splits);
@@ -323,6 +369,9 @@ static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
         case 2: return pick_in<Fam<4>>(d, false, f);  // 4-row stages (C22: 92 KB LDS, 1 block/CU)
         case 3: return pick_in<Fam<4>>(d, true, f);   // 4-row stages, 32-cout tiles (<= 75 KB)
         case 4: return f(Fam<8>::C11());              // 8-row stages, 32x32 tiles
+        case 5: return f(Fam<8, 2>::C11());           // variant 4 with 2 waves per kernel row (K split)
+        case 6: return f(Fam<4, 2>::C11());           // 4-row stages, 2 waves per kernel row
+        case 7: return f(Fam<8, 2>::C12());           // 32x64 tiles, 2 waves per kernel row
         default:
             // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles with
             // 8-row stages, or 4-row stages when cin % 64 == 32 (96, 160): 11-19 % over variant 1
