@@ -49,7 +49,8 @@ class IsrTailDesc(ctypes.Structure):
 class IsrWgradDesc(ctypes.Structure):
     _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
                 ("cin", c_int32), ("cout", c_int32), ("x", IsrView), ("g", IsrView), ("g_sub2", c_int32),
-                ("scale", c_float), ("dw", c_void_p), ("db", c_void_p), ("splits", c_int32)]
+                ("scale", c_float), ("dw", c_void_p), ("db", c_void_p), ("splits", c_int32),
+                ("x_sub2", c_int32), ("taps", c_int32)]
 
 
 class IsrWgrad9Desc(ctypes.Structure):

@@ -179,10 +179,14 @@ static int conv3x3_validate(const isr_conv_desc* d) {
         return ISR_ERR_BAD_DESC;
     }
     if (d->m.data) {
-        if (d->shuffle != 1 || d->y2.data)
-            return fail(ISR_ERR_UNSUPPORTED, "conv3x3: mask epilogue takes no shuffle / second output");
+        if (d->y2.data) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: mask epilogue takes no second output");
         if (d->m_c0 < 0 || d->m_c0 % 32) return fail(ISR_ERR_BAD_DESC, "conv3x3: m_c0 %d must be a multiple of 32", d->m_c0);
-        if (!view_ok(d->m, d->ha, d->wa, 0, d->cout, "conv3x3.m", 1)) return ISR_ERR_BAD_DESC;
+        if (d->shuffle == 2) {  // mask read on the shuffled (2h x 2w) grid, every channel
+            if (d->m_c0) return fail(ISR_ERR_UNSUPPORTED, "conv3x3: a shuffled store masks all channels (m_c0 = 0)");
+            if (!view_ok(d->m, 2 * d->ha, 2 * d->wa, 0, d->cout / 4, "conv3x3.m", 1)) return ISR_ERR_BAD_DESC;
+        } else if (!view_ok(d->m, d->ha, d->wa, 0, d->cout, "conv3x3.m", 1)) {
+            return ISR_ERR_BAD_DESC;
+        }
     }
     if (d->r1_cn < 0 || d->r1_cn % 32) return fail(ISR_ERR_BAD_DESC, "conv3x3: r1_cn %d must be a multiple of 32", d->r1_cn);
     if (d->shuffle == 2) {
@@ -248,7 +252,14 @@ static int wgrad_validate(const isr_wgrad_desc* d) {
         return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: cin %d / cout %d must be multiples of 32", d->cin, d->cout);
     if (!d->dw) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null dw");
     if (d->splits < 0) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: negative split count");
-    if (!view_ok(d->x, d->ha, d->wa, 1, d->cin, "wgrad3x3.x", 1)) return ISR_ERR_BAD_DESC;
+    if (d->taps < 0 || d->taps > 1) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: taps must be 0 or 1");
+    if (d->x_sub2) {
+        if (d->cin % 128) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: x_sub2 needs cin %% 128 == 0 (got %d)", d->cin);
+        if (d->g_sub2) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: x_sub2 with g_sub2");
+        if (!view_ok(d->x, 2 * d->ha, 2 * d->wa, 2, d->cin / 4, "wgrad3x3.x", 1)) return ISR_ERR_BAD_DESC;
+    } else if (!view_ok(d->x, d->ha, d->wa, 1, d->cin, "wgrad3x3.x", 1)) {
+        return ISR_ERR_BAD_DESC;
+    }
     if (d->g_sub2) {
         if (d->cout % 128) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: g_sub2 needs cout %% 128 == 0");
         if (!view_ok(d->g, 2 * d->ha, 2 * d->wa, 0, d->cout / 4, "wgrad3x3.g", 1)) return ISR_ERR_BAD_DESC;

@@ -119,6 +119,13 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
                     v[k] = ep[xc * EPS + 4 * (cg * 8 + k) + 2 * si + sj];
                     v[k] = v[k] >= 0.f ? v[k] : v[k] * slope;
                 }
+                if constexpr (MODE & 16) {  // LeakyReLU' of the (shuffled-grid) mask source, all channels
+                    const bf16x8 mq =
+                        *reinterpret_cast<const bf16x8*>(view_at(d.m, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8));
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (!((float)mq[k] > 0.f)) v[k] *= d.mslope;
+                }
                 if (!(yy < d.h && x0 + xc < d.w)) {
 #pragma unroll
                     for (int k = 0; k < 8; ++k) v[k] = 0.f;
@@ -399,7 +406,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         return;
     }
     // ---- epilogue (mode picked once, wave-uniform, so no per-element branches)
-    const int mode = d.shuffle == 2 ? 8
+    const int mode = d.shuffle == 2 ? (d.m.data ? 24 : 8)
                                     : ((d.r1.data ? 1 : 0) | (d.r2.data ? 2 : 0) | (d.y2.data ? 4 : 0) | (d.m.data ? 16 : 0));
     switch (mode) {
         case 0: epilogue<C, 0>(d, acc, img, ct, x0, y0, wave, lane); break;
@@ -411,6 +418,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         case 6: epilogue<C, 6>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 7: epilogue<C, 7>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 8: epilogue<C, 8>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 24: epilogue<C, 24>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 16: epilogue<C, 16>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 17: epilogue<C, 17>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 18: epilogue<C, 18>(d, acc, img, ct, x0, y0, wave, lane); break;

@@ -39,13 +39,15 @@ __device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int NCO_, int NCI_, int TY_, int KW_ = 1>
+template <int NCO_, int NCI_, int TY_, int KW_ = 1, int TWN_ = 0>
 struct WG {
     static constexpr int NCO = NCO_, NCI = NCI_, TY = TY_;
+    // tap window: 0 = 3x3; 1 = taps {0,1}^2 (2 kernel rows, 2 columns: stride-2 phase convs)
+    static constexpr int TWN = TWN_, TN = TWN_ ? 2 : 3;
     // KW waves per kernel row dy split each stage's K (pixel groups) between them;
     // their partial sums are added through LDS before the workspace store
     static constexpr int KW = KW_;
-    static constexpr int WM = 3 * KW, NT = 64 * WM;
+    static constexpr int WM = TN * KW, NT = 64 * WM;
     static constexpr int CO_T = 32 * NCO, CI_T = 32 * NCI;
     static constexpr int GPL = 2 * NCO, XPL = 2 * NCI;         // 16-channel planes per stage
     static constexpr int XPIX = (TY + 2) * 34;                  // halo pixels per plane
@@ -59,7 +61,7 @@ struct WG {
     static constexpr int STAGE = G_BYTES + XPL * X_PLANE;
     static constexpr int G_INSTR = GPL * G_IPL, INSTR = G_INSTR + XPL * X_IPL;
     static constexpr int IPW = (INSTR + WM - 1) / WM;
-    static constexpr int RED = (KW - 1) * 3 * 64 * (3 * NCO * NCI * 16 + NCO) * 4;  // cross-wave K reduction
+    static constexpr int RED = (KW - 1) * TN * 64 * (TN * NCO * NCI * 16 + NCO) * 4;  // cross-wave K reduction
     static constexpr int LDS = 2 * STAGE > RED ? 2 * STAGE : RED;
     static_assert(LDS <= 163840, "LDS budget");
     static_assert((2 * TY) % KW == 0, "K groups split evenly between the KW waves of a row");
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
     const int split = b;
     const int t0 = (int)((long)split * a.tiles / a.splits), t1 = (int)((long)(split + 1) * a.tiles / a.splits);
     const int wave = wave_id();
-    const int dy = wave % 3, kh = wave / 3;  // kernel row, K-share of this wave
+    const int dy = wave % C::TN, kh = wave / C::TN;  // kernel row, K-share of this wave
     const int lane = threadIdx.x & 63;
     const int nbx = d.wa / 32, nby = d.ha / TY;
 
@@ -113,7 +115,14 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
             int q = u >> 1;
             if (q >= C::XPIX) q = 0;  // tail lanes of the last instruction: harmless duplicate
             const int row = q / 34, col = q - row * 34;
-            o = (uint32_t)((size_t)((cit * C::CI_T) / 16 + pl) * xps + (size_t)row * xrow + col * 32 + (u & 1) * 16);
+            if (d.x_sub2) {  // kernel channel c' = s*(cin/4) + c  →  x pixel (2row + (s>>1), 2col + (s&1)), channel c
+                const int cpr = cit * C::CI_T + pl * 16, xs4 = d.cin >> 2;
+                const int sp = cpr / xs4, c = cpr - sp * xs4;
+                o = (uint32_t)((size_t)(c >> 4) * xps + (size_t)(2 * row + (sp >> 1)) * xrow + (2 * col + (sp & 1)) * 32 +
+                               (u & 1) * 16);
+            } else {
+                o = (uint32_t)((size_t)((cit * C::CI_T) / 16 + pl) * xps + (size_t)row * xrow + col * 32 + (u & 1) * 16);
+            }
         }
         off[k] = o;
     }
@@ -133,7 +142,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         const int x0 = bx * 32, y0 = by * TY;
         // view_at with channel 0: the per-lane offsets carry the plane / sub-position
         const char* gb = d.g_sub2 ? view_at(d.g, img, 2 * y0, 2 * x0, 0) : view_at(d.g, img, y0, x0, 0);
-        const char* xb = view_at(d.x, img, y0 - 1, x0 - 1, 0);
+        const char* xb = d.x_sub2 ? view_at(d.x, img, 2 * (y0 - 1), 2 * (x0 - 1), 0) : view_at(d.x, img, y0 - 1, x0 - 1, 0);
         char* dst = smem + buf * C::STAGE;
 #pragma unroll
         for (int k = 0; k < C::IPW; ++k) {
@@ -142,9 +151,9 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         }
     };
 
-    f32x16 acc[3][NCO][NCI];
+    f32x16 acc[C::TN][NCO][NCI];
 #pragma unroll
-    for (int dx = 0; dx < 3; ++dx)
+    for (int dx = 0; dx < C::TN; ++dx)
 #pragma unroll
         for (int f = 0; f < NCO; ++f)
 #pragma unroll
@@ -186,7 +195,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
                     for (int e = 0; e < 8; ++e) bsum[f] += (float)fa[f][e];
             }
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx) {
+            for (int dx = 0; dx < C::TN; ++dx) {
                 bf16x8 fb[NCI];
 #pragma unroll
                 for (int e = 0; e < NCI; ++e) {
@@ -205,13 +214,13 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         // add the K-shares of the KW waves of each kernel row (through the now idle stage LDS)
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __syncthreads();
-        constexpr int PER = 3 * NCO * NCI * 16 + NCO;  // floats per lane
+        constexpr int PER = C::TN * NCO * NCI * 16 + NCO;  // floats per lane
         float* red = reinterpret_cast<float*>(smem);
         if (kh > 0) {
-            float* dst = red + ((size_t)((kh - 1) * 3 + dy) * 64 + lane) * PER;
+            float* dst = red + ((size_t)((kh - 1) * C::TN + dy) * 64 + lane) * PER;
             int q = 0;
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
+            for (int dx = 0; dx < C::TN; ++dx)
 #pragma unroll
                 for (int f = 0; f < NCO; ++f)
 #pragma unroll
@@ -225,10 +234,10 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         if (kh > 0) return;
 #pragma unroll
         for (int k = 1; k < C::KW; ++k) {
-            const float* src = red + ((size_t)((k - 1) * 3 + dy) * 64 + lane) * PER;
+            const float* src = red + ((size_t)((k - 1) * C::TN + dy) * 64 + lane) * PER;
             int q = 0;
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx)
+            for (int dx = 0; dx < C::TN; ++dx)
 #pragma unroll
                 for (int f = 0; f < NCO; ++f)
 #pragma unroll
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
     const int l31 = lane & 31;
     float* wsp = a.ws + (size_t)split * (9 * d.cout * d.cin + d.cout);
 #pragma unroll
-    for (int dx = 0; dx < 3; ++dx) {
+    for (int dx = 0; dx < C::TN; ++dx) {
         float* wt = wsp + (size_t)(dy * 3 + dx) * d.cout * d.cin;
 #pragma unroll
         for (int f = 0; f < NCO; ++f)
@@ -373,6 +382,7 @@ static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
         case 6: return f(Fam<4, 2>::C11());           // 4-row stages, 2 waves per kernel row
         case 7: return f(Fam<8, 2>::C12());           // 32x64 tiles, 2 waves per kernel row
         default:
+            if (d->taps == 1) return f(WG<1, 1, 8, 2, 1>());  // stride-2 phase conv: taps {0,1}^2, 4 waves
             // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles with
             // 8-row stages, or 4-row stages when cin % 64 == 32 (96, 160): 11-19 % over variant 1
             if (d->cin % 64 == 32) return f(Fam<4>::C11());

@@ -13,7 +13,8 @@ Stride 2 on the stride-1 kernel, exactly (no zero taps beyond a 2x2 window):
             W''[4c+s][co][ty][tx] = W[co][c][dy][dx] on taps {1,2}²
             (a=0: ty=1↔dy=1; a=1: ty=2↔dy=0, ty=1↔dy=2), stored through the
             PixelShuffle(2) epilogue;
-  wgrad     on the materialised unshuffled input, dW gathered from dW'.
+  wgrad     over the x_sub2 view on taps {0,1}² (isr_wgrad_desc.x_sub2 / taps),
+            dW gathered from dW'.
 The first layer's 3 input channels are zero-padded to 32 (the wgrad K tile).
 Activations are bf16 channel-blocked (ops.ActBuffer), accumulation fp32, BN
 statistics in double (isr_bn_*).
@@ -122,7 +123,7 @@ class DiscriminatorPlan:
             return 0, 0
 
         self.xin = ActBuffer.alloc(n, h, w, L[0].cin_p, 1, dev)
-        self.A, self.Z, self.gA, self.dZ, self.U = [], [], [], [], []
+        self.A, self.Z, self.gA, self.dZ = [], [], [], []
         for i, l in enumerate(L):
             p = pad_of(i)
             mh, mw = slack(i, p)
@@ -134,8 +135,6 @@ class DiscriminatorPlan:
             self.gA.append(ActBuffer.alloc(n, *res[i], l.cout, 1, dev, ha=ha[i], wa=wa[i], min_hp=gh, min_wp=gwd))
             self.dZ.append(ActBuffer.alloc(n, *res[i], l.cout, 1, dev, ha=ha[i], wa=wa[i]) if l.bn is not None
                            else None)
-            self.U.append(ActBuffer.alloc(n, *res[i], 4 * l.cin, 1, dev, ha=ha[i], wa=wa[i]) if l.stride == 2
-                          else None)
             if l.bn is not None:
                 l.bn_state = ops.BNState(l.cout, dev)
         self.gin = ActBuffer.alloc(n, h, w, 32, 0, dev)  # layer-0 input gradient (3 of 32 channels used)
@@ -209,18 +208,10 @@ class DiscriminatorPlan:
                 g = self.dZ[i]
             xin = self.A[i - 1] if i > 0 else self.xin
             # weight (+ bias) gradient
-            if l.stride == 2:
-                U = self.U[i]
-                hi, wi = self.res[i]
-                pa = xin.pad
-                cb = l.cin // 16
-                for a in (0, 1):
-                    for b in (0, 1):
-                        s = 2 * a + b
-                        U.t[:, s * cb:(s + 1) * cb, 1:1 + hi, 1:1 + wi, :] = \
-                            xin.t[:, :, pa + a:pa + 2 * hi:2, pa + b:pa + 2 * wi:2, :]
+            if l.stride == 2:  # phase-decomposed: x read through the x_sub2 view, taps {0,1}^2
                 dwp = torch.empty(l.cout, 4 * l.cin, 3, 3, device=self.device)
-                self._wgrad(U, 4 * l.cin, g, l.cout, dwp, None)
+                ops.launch_wgrad3x3(ops.wgrad3x3_desc(xin, 4 * l.cin, g, l.cout, dwp, None, x_sub2=True, taps=1),
+                                    self.device)
                 gw.append(gather_wgrad(dwp, l.cin))
             else:
                 dw = torch.empty(l.cout, l.cin_p, 3, 3, device=self.device)
@@ -235,8 +226,8 @@ class DiscriminatorPlan:
             # input gradient
             if i > 0:
                 if l.stride == 2:
-                    ops.conv3x3(g, l.cout, l.bwd, None, 4 * l.cin, self.gA[i - 1], slope=1.0, shuffle=2, taps=2)
-                    ops.ew_combine(self.gA[i - 1], self.gA[i - 1], l.cin, m=self.A[i - 1], mslope=SLOPE)
+                    ops.conv3x3(g, l.cout, l.bwd, None, 4 * l.cin, self.gA[i - 1], slope=1.0, shuffle=2, taps=2,
+                                m=self.A[i - 1], mslope=SLOPE)
                 else:
                     ops.conv3x3(g, l.cout, l.bwd, None, l.cin, self.gA[i - 1], m=self.A[i - 1], mslope=SLOPE)
         dx = None

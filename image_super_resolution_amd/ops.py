@@ -315,15 +315,19 @@ _WS = Workspace()
 
 def wgrad3x3_desc(x: ActBuffer, cin: int, g: ActBuffer, cout: int, dw: torch.Tensor, db: torch.Tensor | None = None,
                   *, x_coff: int = 0, g_coff: int = 0, scale: float = 1.0, g_sub2: bool = False,
-                  splits: int = 0) -> IsrWgradDesc:
-    """dw[cout, cin, 3, 3] = scale * sum g ⊗ shifted x (fp32, overwritten); db[cout] likewise."""
+                  splits: int = 0, x_sub2: bool = False, taps: int = 0) -> IsrWgradDesc:
+    """dw[cout, cin, 3, 3] = scale * sum g ⊗ shifted x (fp32, overwritten); db[cout] likewise.
+    `x_sub2`: x (2h x 2w grid) is read as PixelShuffle(2)ᵀ (cin = 4 x its channels);
+    `taps=1`: only taps {0,1}² are computed (stride-2 phase convs)."""
     if dw.dtype != torch.float32 or not dw.is_contiguous() or tuple(dw.shape) != (cout, cin, 3, 3):
         raise ValueError("wgrad3x3: dw must be contiguous fp32 [cout, cin, 3, 3]")
     if db is not None and (db.dtype != torch.float32 or not db.is_contiguous() or db.numel() != cout):
         raise ValueError("wgrad3x3: db must be contiguous fp32 [cout]")
     d = IsrWgradDesc()
-    d.n, d.h, d.w, d.ha, d.wa = x.n, x.h, x.w, x.ha, x.wa
+    grid = g if x_sub2 else x
+    d.n, d.h, d.w, d.ha, d.wa = grid.n, grid.h, grid.w, grid.ha, grid.wa
     d.cin, d.cout = cin, cout
+    d.x_sub2, d.taps = int(bool(x_sub2)), taps
     d.x = x.view(x_coff)
     d.g = g.view(g_coff)
     d.g_sub2 = int(bool(g_sub2))

@@ -79,7 +79,8 @@ typedef struct isr_conv_desc {
      * of train.py:57 / :102): input-gradient convs accumulate into the dense-block
      * gradient buffer and apply LeakyReLU' of the forward activation. */
     isr_view m;        /* optional mask source (data == NULL → none), same grid as y */
-    float mslope;      /* output channel c >= m_c0 is multiplied by (m[c] > 0 ? 1 : mslope) */
+    float mslope;      /* output channel c >= m_c0 is multiplied by (m[c] > 0 ? 1 : mslope); with shuffle == 2
+                          m is on the shuffled grid and masks every channel (m_c0 = 0) */
     int32_t m_c0;      /* first masked output channel, multiple of 32 */
     int32_t r1_cn;     /* r1 is added only to output channels < r1_cn (0 → all); multiple of 32 */
     int32_t x_sub2;    /* 1: input channel c' = s*(cin/4) + c reads x at pixel (2y + (s>>1), 2x + (s&1)),
@@ -146,6 +147,11 @@ typedef struct isr_wgrad_desc {
     float* dw;               /* [cout][cin][3][3] fp32 */
     float* db;               /* [cout] fp32 or NULL */
     int32_t splits;          /* split-K count; 0 = library choice */
+    int32_t x_sub2;          /* 1: x is read as PixelShuffle(2)^T of a 2h x 2w buffer (pad >= 2): kernel input
+                                channel s*(cin/4) + c = x[c] at (2y + (s>>1), 2x + (s&1)); cin % 128 == 0.
+                                With taps == 1 this is the weight gradient of a stride-2 conv (Discriminator,
+                                utils/models.py:533-542) on its phase decomposition. */
+    int32_t taps;            /* 0: all 3x3 taps; 1: only taps {0,1}^2 (dw at other taps left undefined) */
 } isr_wgrad_desc;
 
 /* Weight / bias gradients of the 9x9 convs (same workspace contract):

@@ -64,6 +64,20 @@ def test_stride2_conv_forward_dgrad_wgrad(cin, cout, h, w):
     ops.wgrad3x3(U, 4 * cin, gyb, cout, dwp, None)
     torch.cuda.synchronize()
     assert _rel(D.gather_wgrad(dwp, cin), Wr.grad) < 1e-3
+    # ... and straight from the full-resolution buffer through the x_sub2 view, taps {0,1}^2 only
+    dwq = torch.empty(cout, 4 * cin, 3, 3, device=DEV)
+    ops.wgrad3x3(xb, 4 * cin, gyb, cout, dwq, None, x_sub2=True, taps=1)
+    torch.cuda.synchronize()
+    assert _rel(D.gather_wgrad(dwq, cin), Wr.grad) < 1e-3
+    # input gradient with the LeakyReLU' mask fused into the PixelShuffle epilogue
+    act = bf(torch.randn(2, cin, h, w, generator=g)).to(DEV)
+    mb = ops.ActBuffer.alloc(2, h, w, cin, 0, DEV, min_hp=2 * gyb.ha, min_wp=2 * gyb.wa)
+    mb.set_nchw(act, 0)
+    gmb = ops.ActBuffer.alloc(2, h, w, cin, 1, DEV, min_hp=2 * gyb.ha + 2, min_wp=2 * gyb.wa + 2)
+    ops.conv3x3(gyb, cout, ops.pack_conv3x3(D.expand_dgrad(W)), None, 4 * cin, gmb, shuffle=2, taps=2, m=mb,
+                mslope=0.2)
+    torch.cuda.synchronize()
+    assert _rel(gmb.to_nchw(), xr.grad * torch.where(act > 0, 1.0, 0.2)) < 1e-2
 
 
 def _pair(seed):
