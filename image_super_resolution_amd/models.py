@@ -397,12 +397,13 @@ def sliding_window(image: torch.Tensor, step, windowSize=None):
 
 
 class Discriminator(nn.Module):
-    """SRGAN discriminator (utils/models.py:513-569).  `use_libisr(True)` runs the
-    eight conv blocks in train mode (incl. the stride-2 ones and train-mode
-    BatchNorm) on libisr (discriminator.py); the adaptive pool and the two Linear
-    layers are torch ops either way.  Off by default: at [16,3,512,512] the libisr
-    stack (10.6 ms fwd+bwd, its stride-2 wgrad still computes all 9 phase taps) is
-    slower than MIOpen in NHWC with find mode (8.9 ms, tools/bench_disc.py)."""
+    """SRGAN discriminator (utils/models.py:513-569).  In train mode on the GPU the
+    eight conv blocks (incl. the stride-2 ones and train-mode BatchNorm) run on
+    libisr (discriminator.py); the adaptive pool and the two Linear layers are
+    torch ops.  `use_libisr(False)` (or eval mode) runs the stock modules: at
+    [16,3,512,512] the libisr stack is at parity with MIOpen NHWC + find mode
+    (8.5-8.8 vs 8.5-9.2 ms fwd+bwd, tools/bench_disc.py), 2 % faster in the full
+    SRGAN step, and needs no MIOpen kernel search at start-up."""
 
     def __init__(self, kernel_size=3, n_channels=64, n_blocks=8, fc_size=1024):
         super().__init__()
@@ -428,7 +429,7 @@ class Discriminator(nn.Module):
 
     def forward(self, inputs):
         b = inputs.size(0)
-        if self.training and inputs.is_cuda and self.__dict__.get("hip", False):
+        if self.training and inputs.is_cuda and self.__dict__.get("hip", True):
             from .discriminator import conv_stack_train
             feat = conv_stack_train(self, inputs)
         else:

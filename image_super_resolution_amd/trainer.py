@@ -10,8 +10,9 @@ Differences, all deliberate:
 * bf16 storage with fp32 accumulation and fp32 master weights replaces fp16
   autocast, so the GradScaler is disabled (bf16 has fp32's exponent range);
   the GradScaler objects are kept for checkpoint compatibility.
-* the discriminator (stock PyTorch-ROCm ops) runs under bf16
-  autocast where the reference uses fp16 autocast (train.py:91, :114).
+* the discriminator's conv stack runs on libisr (discriminator.py, bf16 storage,
+  fp32 accumulation); its pool + Linear head under bf16 autocast where the
+  reference uses fp16 autocast (train.py:91, :114).
 * Adam (optim.FusedAdam, built by train.py), clip_grad_norm_ and the EMA update
   run as one HIP multi-tensor launch each (optim.py) instead of per-tensor loops.
 * loss.item() host syncs happen once per `log_every` iterations instead of

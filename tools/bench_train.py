@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--mode", default="srgan", choices=["srgan", "pixel"])
     ap.add_argument("--dis-layout", default="nhwc", choices=["nchw", "nhwc"],
                     help="discriminator memory format (stock MIOpen convs)")
-    ap.add_argument("--dis-libisr", action="store_true", help="discriminator conv stack on libisr")
+    ap.add_argument("--dis-miopen", action="store_true", help="discriminator conv stack on stock MIOpen convs")
     ap.add_argument("--no-miopen-find", dest="miopen_find", action="store_false",
                     help="torch.backends.cudnn.benchmark = False (default: MIOpen find mode on, as train.py)")
     args = ap.parse_args()
@@ -54,10 +54,10 @@ def main():
     if args.mode == "srgan":
         gen = models.SRGAN(args.blocks, 0.2, True, 4).to(dev)
         dis = models.Discriminator(3, 64, 8, 1024).to(dev)
-        dis.use_libisr(args.dis_libisr)
-        if args.dis_layout == "nhwc":
+        dis.use_libisr(not args.dis_miopen)
+        if args.dis_miopen and args.dis_layout == "nhwc":
             dis = dis.to(memory_format=torch.channels_last)
-        torch.backends.cudnn.benchmark = args.miopen_find
+        torch.backends.cudnn.benchmark = args.miopen_find and args.dis_miopen
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             gl = L.gen_loss(device=dev, beforeAct=True)
@@ -108,7 +108,7 @@ def main():
                           "value": round(samples * args.hr * args.hr / 1e6 / dt, 2), "unit": "HR MPix/s",
                           "samples_per_s": round(samples / dt, 2), "ms_per_step": round(dt * 1e3 / args.steps, 2),
                           "n_gpus": world, "global_batch": args.batch * world, "steps": args.steps,
-                          "dis_layout": args.dis_layout, "miopen_find": args.miopen_find,
+                          "discriminator": "miopen" if args.dis_miopen else "libisr",
                           "mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -138,7 +138,7 @@ def main(opt):
     else:
         gen_net = models.SRGAN(opt.rs_deep, opt.add_rate, opt.enchant, opt.scale)
         gen_net.init_weight(pretrained=res_ck.as_posix())
-        dis_net = models.Discriminator(3, 64, 8, 1024).use_libisr(opt.dis_libisr)
+        dis_net = models.Discriminator(3, 64, 8, 1024).use_libisr(not opt.dis_miopen)
         ema = models.ModelEMA(gen_net, tau=opt.epochs * iters)
         optimizer_g = optim.FusedAdam(gen_net.parameters(), lr=opt.lr, betas=(0.9, 0.999),
                                        weight_decay=opt.weight_decay)
@@ -161,10 +161,11 @@ def main(opt):
             start = ck["epoch"] + 1
         compute_loss = L.gen_loss(device=device, beforeAct=opt.enchant, vgg_weights=opt.vgg_weights)
         gen_net.to(device)
-        # the discriminator stays on stock MIOpen convs: NHWC (channels_last) + find mode
-        # (cudnn.benchmark) cut its share of the step by ~17 % vs NCHW (tools/bench_train.py)
-        dis_net.to(device, memory_format=torch.channels_last)
-        torch.backends.cudnn.benchmark = True
+        if opt.dis_miopen:  # stock convs: NHWC (channels_last) + find mode, ~17 % faster than NCHW
+            dis_net.to(device, memory_format=torch.channels_last)
+            torch.backends.cudnn.benchmark = True
+        else:
+            dis_net.to(device)
         ema.ema.to(device)
         if group is not None:
             enable_grad_allreduce(gen_net, group)
@@ -222,8 +223,8 @@ def parse(argv=None):
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--steps", type=int, default=0, help="iterations per epoch (0 = one pass over the data)")
     p.add_argument("--vgg_weights", type=str, default=None)
-    p.add_argument("--dis_libisr", action="store_true", help="run the discriminator's conv stack on libisr "
-                   "(default: MIOpen NHWC, currently faster; DESIGN.md §8)")
+    p.add_argument("--dis_miopen", action="store_true", help="run the discriminator's conv stack on stock MIOpen "
+                   "convs (NHWC + find mode) instead of libisr")
     opt = p.parse_args(argv)
     if not opt.data and Path("train_images.json").is_file():
         opt.data = "train_images.json"
