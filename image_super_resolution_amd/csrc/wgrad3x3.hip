@@ -328,16 +328,19 @@ struct Fam {
     using C11 = WG<1, 1, TY, KW>;
 };
 
-static int wgrad_splits(const isr_wgrad_desc* d, int tiles, int pairs) {
+static int wgrad_splits(const isr_wgrad_desc* d, int tiles, int pairs, int target) {
     if (d->splits > 0) return d->splits < tiles ? d->splits : tiles;
-    int s = (640 + pairs - 1) / pairs;
+    int s = (target + pairs - 1) / pairs;
     return s < tiles ? s : tiles;
 }
 
 template <class C>
 static void wgrad_geometry(const isr_wgrad_desc* d, int* tiles, int* splits) {
     *tiles = d->n * (d->ha / C::TY) * (d->wa / 32);
-    *splits = wgrad_splits(d, *tiles, (d->cout / C::CO_T) * (d->cin / C::CI_T));
+    // ~640 blocks of <= 6 waves; blocks with more K-share waves need proportionally fewer
+    // splits (each split-K partial costs a workspace write + reduce read)
+    const int target = C::KW > 2 ? 640 * 2 / C::KW : 640;
+    *splits = wgrad_splits(d, *tiles, (d->cout / C::CO_T) * (d->cin / C::CI_T), target);
 }
 
 template <class C>
@@ -381,11 +384,17 @@ static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
         case 5: return f(Fam<8, 2>::C11());           // variant 4 with 2 waves per kernel row (K split)
         case 6: return f(Fam<4, 2>::C11());           // 4-row stages, 2 waves per kernel row
         case 7: return f(Fam<8, 2>::C12());           // 32x64 tiles, 2 waves per kernel row
+        case 8: return f(Fam<8, 4>::C11());           // 4 waves per kernel row (12 per block), half the splits
+        case 9: return f(Fam<16, 4>::C11());          // 16-row stages, 4 waves per kernel row
+        case 10: return f(Fam<4, 4>::C11());          // 4-row stages, 4 waves per kernel row
+        case 11: return f(Fam<16, 2>::C11());         // 16-row stages, 2 waves per kernel row
         default:
             if (d->taps == 1) return f(WG<1, 1, 8, 2, 1>());  // stride-2 phase conv: taps {0,1}^2, 4 waves
-            // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles with
-            // 8-row stages, or 4-row stages when cin % 64 == 32 (96, 160): 11-19 % over variant 1
+            // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles; 4-row
+            // stages when cin % 64 == 32 (96, 160), else 16-row stages with 4 waves per kernel
+            // row (12-wave blocks, half the split-K partials): 8-11 % over 8-row stages
             if (d->cin % 64 == 32) return f(Fam<4>::C11());
+            if (d->ha % 16 == 0) return f(Fam<16, 4>::C11());
             return f(Fam<8>::C11());
     }
 }
