@@ -190,7 +190,10 @@ class DiscriminatorPlan:
     def _wgrad(self, x: ActBuffer, cin: int, g: ActBuffer, cout: int, dw: torch.Tensor, db) -> None:
         ops.launch_wgrad3x3(ops.wgrad3x3_desc(x, cin, g, cout, dw, db), self.device)
 
-    def backward(self, gfeat: torch.Tensor, need_input_grad: bool) -> tuple[torch.Tensor | None, list]:
+    def backward(self, gfeat: torch.Tensor, need_input_grad: bool,
+                 need_param_grads: bool = True) -> tuple[torch.Tensor | None, list]:
+        """Input gradient and parameter gradients (all None when `need_param_grads`
+        is False: the weight-gradient convs are skipped, only dgrad runs)."""
         L = self.layers
         last = len(L) - 1
         # gradient wrt the last activation → wrt its BN output (LeakyReLU')
@@ -208,7 +211,9 @@ class DiscriminatorPlan:
                 g = self.dZ[i]
             xin = self.A[i - 1] if i > 0 else self.xin
             # weight (+ bias) gradient
-            if l.stride == 2:  # phase-decomposed: x read through the x_sub2 view, taps {0,1}^2
+            if not need_param_grads:
+                gw = [None] * (2 if l.b is not None else 1)
+            elif l.stride == 2:  # phase-decomposed: x read through the x_sub2 view, taps {0,1}^2
                 dwp = torch.empty(l.cout, 4 * l.cin, 3, 3, device=self.device)
                 ops.launch_wgrad3x3(ops.wgrad3x3_desc(xin, 4 * l.cin, g, l.cout, dwp, None, x_sub2=True, taps=1),
                                     self.device)
@@ -221,7 +226,7 @@ class DiscriminatorPlan:
                 if db is not None:
                     gw.append(db)
             if l.bn is not None:
-                gw += [dgam, dbet]
+                gw += [dgam, dbet] if need_param_grads else [None, None]
             grads[i] = gw
             # input gradient
             if i > 0:
@@ -268,7 +273,7 @@ class _DiscFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gfeat):
         plan = ctx.lease.plan
-        dx, grads = plan.backward(gfeat.contiguous(), ctx.needs_input_grad[0])
+        dx, grads = plan.backward(gfeat.contiguous(), ctx.needs_input_grad[0], any(ctx.needs_input_grad[2:]))
         ctx.lease.release()
         return (dx, None, *grads)
 

@@ -15,6 +15,8 @@ Differences, all deliberate:
   reference uses fp16 autocast (train.py:91, :114).
 * Adam (optim.FusedAdam, built by train.py), clip_grad_norm_ and the EMA update
   run as one HIP multi-tensor launch each (optim.py) instead of per-tensor loops.
+* the discriminator's parameters are frozen during the generator-loss forward,
+  so its discarded parameter gradients (train.py:102, zeroed at :119) are not computed.
 * loss.item() host syncs happen once per `log_every` iterations instead of
   every iteration (train.py:64-65, :101-112).
 * multi-GPU (one process per GPU): the generator's gradients are averaged by
@@ -24,6 +26,7 @@ Differences, all deliberate:
 """
 from __future__ import annotations
 
+import contextlib
 import time
 
 import torch
@@ -39,6 +42,19 @@ def _scalar(writer, tag, value, step):
 
 def _unwrap(m):
     return m.module if hasattr(m, "module") else m
+
+
+@contextlib.contextmanager
+def _frozen(module):
+    """requires_grad=False on `module`'s trainable parameters for the graphs built inside."""
+    ps = [p for p in module.parameters() if p.requires_grad]
+    for p in ps:
+        p.requires_grad_(False)
+    try:
+        yield
+    finally:
+        for p in ps:
+            p.requires_grad_(True)
 
 
 def train(model, ema: ModelEMA, batches, transform, compute_loss, optimizer, gradscaler, schedule, epoch: int,
@@ -91,9 +107,11 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
         sr_images = gen_net(lr_images)
         sr_images = (sr_images + 1.0) / 2.0
         sr_images = (sr_images - mean) / std
-        # the discriminator's gradients from the generator loss are discarded
-        # (optimizer_d.zero_grad below), exactly as in the reference
-        with torch.autocast("cuda", dtype=torch.bfloat16):  # the reference runs D under fp16 autocast
+        # the reference computes the discriminator's parameter gradients from the
+        # generator loss and then discards them (optimizer_d.zero_grad, train.py:119);
+        # D's parameters are frozen for this forward so only its input gradient is
+        # computed — same parameter updates, one weight-gradient pass fewer
+        with torch.autocast("cuda", dtype=torch.bfloat16), _frozen(dis_net):  # reference: fp16 autocast
             sr_discriminated = dis_net(sr_images)
         perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(sr_images, hr_images,
                                                                                          sr_discriminated)

@@ -136,3 +136,21 @@ def test_two_live_graphs_use_separate_plans():
         assert _rel(ph.grad, pr.grad) <= 1.3 * _rel(pa.grad, pr.grad) + 0.02
     plans = next(iter(hip.__dict__["_isr_plans"].values()))
     assert len(plans) == 2 and not any(p.busy for p in plans)
+
+
+def test_frozen_parameters_skip_weight_gradients():
+    """trainer.train_srgan freezes D for the generator-loss forward: the input
+    gradient is unchanged and no parameter gradient is produced."""
+    from image_super_resolution_amd import trainer
+    hip, _ = _pair(2)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 3, 64, 64, generator=g).to(DEV)
+    _, dx_full, _ = _run(hip, x, 1.0)
+    hip.zero_grad(set_to_none=True)
+    xr = x.clone().requires_grad_()
+    with trainer._frozen(hip):
+        o = hip(xr)
+    assert all(p.requires_grad for p in hip.parameters())
+    o.float().sum().backward()
+    assert torch.equal(xr.grad, dx_full)
+    assert all(p.grad is None for p in hip.parameters())

@@ -18,7 +18,7 @@ from pathlib import Path
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-from image_super_resolution_amd import data, loss as L, models, optim  # noqa: E402
+from image_super_resolution_amd import data, loss as L, models, optim, trainer  # noqa: E402
 
 
 def main():
@@ -61,7 +61,7 @@ def main():
         sr = gen(lr)
         sr = ((sr + 1.0) / 2.0 - m) / s
         mark("G fwd")
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16), trainer._frozen(dis):
             srd = dis(sr)
         mark("D(sr) fwd")
         perc, adv, content = gl.calc_contentLoss(sr, hr, srd)
