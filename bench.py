@@ -4,12 +4,16 @@
 Workload: ResNet(num_block_resnet=16, add_rate=0.2, scaleRate=4) — the reference's
 RRDB generator (utils/models.py:592-618) — bf16 on the HIP kernels, 16 synthetic
 128x128 LR tiles per GPU → 16 x 512x512 HR, inputs resident in HBM.  One step =
-one generator forward over the batch.  Multi-GPU: one process per GPU, each
+one generator forward over the batch, split over 2 HIP streams (8 tiles each,
+engine.SplitGeneratorPlan; --streams 1 for the single-stream plan).  Multi-GPU: one process per GPU, each
 rank runs its own 16 tiles (tiles are independent: weak scaling, no
 collective on the data path; only the timing uses a MAX all-reduce).
 
 Prints one JSON line (rank 0).  Extra fields:
   roofline      — dominant kernel (conv3x3 192→64, 48 launches per forward):
+                  timed in isolation on a single-stream full-batch plan (same
+                  kernel, full-batch grid; under the split plan two half-batch
+                  launches share the CUs, so their durations are not their own):
                   its 48 launches of one forward replayed back to back on the
                   launch stream between one pair of HIP events (5 rounds, after
                   the timed region), so the per-launch average matches the
@@ -61,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--round", default="r01")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="HIP streams the batch is split over (default engine.DEFAULT_STREAMS)")
     return ap.parse_args()
 
 
@@ -98,7 +104,9 @@ def main():
     lr, hr = synth_lr_batch(n, hw, hw, seed=1234 + rank * n, scale=S)
     x_cpu = normalize(lr)
     x = x_cpu.to(dev).contiguous()
-    plan = engine.get_plan(gw, x, False, (0.485, 0.456, 0.406), (0.229, 0.224, 0.225))
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    plan = engine.get_plan(gw, x, False, mean, std, streams=args.streams)
+    n_streams = len(plan.streams) if isinstance(plan, engine.SplitGeneratorPlan) else 1
     out = torch.empty(plan.out_shape, dtype=plan.out_dtype, device=dev)
 
     for _ in range(args.warmup):
@@ -132,15 +140,19 @@ def main():
     ms = elapsed / args.steps * 1e3
     hr_px = n * (hw * S) * (hw * S)
     mpix_s = world * hr_px * args.steps / elapsed / 1e6
-    # dominant launches inside the network, event-bracketed: an untimed pass of its own
-    # (96 event records cost ~4 % of a step, so they stay out of the timed loop)
+    # The dominant kernel is timed in isolation: the full batch on ONE stream (with the
+    # split plan two half-batch launches share the CUs, so a launch's duration is not
+    # its own).  First its launches inside the network, event-bracketed, in untimed
+    # forwards of their own (96 event records cost ~4 % of a step, so they stay out of
+    # the timed loop) ...
+    iso = plan if n_streams == 1 else engine.GeneratorPlan(gw, n, hw, hw, dev, False, False, mean, std)
     for _ in range(3):
-        plan.run(x, out, around=around)
+        iso.run(x, out, around=around)
     torch.cuda.synchronize()
     in_net_ms = statistics.mean(a.elapsed_time(b) for a, b in pairs)
-    # back-to-back replay of the dominant launches (per-launch time without the
-    # event packets interleaved between every launch)
-    dom = [(fn, d) for fn, d, tag, var in plan.launches if tag == DOMINANT and var is None]
+    # ... then back to back (per-launch time without the event packets interleaved
+    # between every launch)
+    dom = [(fn, d) for fn, d, tag, var in iso.launches if tag == DOMINANT and var is None]
     stream = torch.cuda.current_stream()
     sp = ops._stream()
     rounds = []
@@ -201,7 +213,8 @@ def main():
             "config": {"workload": f"ResNet({args.blocks}, 0.2, scaleRate={S}) RRDB inference, "
                                    f"{hw}x{hw}->{hw * S}x{hw * S}",
                        "global_batch": n * world, "per_gpu_batch": n, "lr_size": hw, "scale": S,
-                       "parallelism": f"dp{world} (independent tile shards)"},
+                       "parallelism": f"dp{world} (independent tile shards)",
+                       "streams_per_gpu": n_streams},
             "roofline": {"bound": "mfma", "kernel": "conv3x3_fwd 192->64 (RDB final conv)",
                          "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,

@@ -90,12 +90,12 @@ BatchRunner = Callable[[torch.Tensor], torch.Tensor]  # uint8 [b,3,h,w] → uint
 
 
 class GeneratorRunner:
-    """uint8 batch runner on the HIP generator: one GeneratorPlan per (b, h, w)."""
+    """uint8 batch runner on the HIP generator: one plan (engine.make_plan) per (b, h, w)."""
 
     def __init__(self, gw: engine.GeneratorWeights, mean, std, device):
         self.gw, self.mean, self.std, self.device = gw, tuple(mean), tuple(std), torch.device(device)
         self.scale = 2 ** len(gw.scalers)
-        self.plans: dict[tuple[int, int, int], engine.GeneratorPlan] = {}
+        self.plans: dict[tuple[int, int, int], object] = {}
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if x.dtype != torch.uint8 or not x.is_cuda:
@@ -103,7 +103,7 @@ class GeneratorRunner:
         n, _, h, w = x.shape
         plan = self.plans.get((n, h, w))
         if plan is None:
-            plan = engine.GeneratorPlan(self.gw, n, h, w, self.device, True, True, self.mean, self.std)
+            plan = engine.make_plan(self.gw, n, h, w, self.device, True, True, self.mean, self.std)
             self.plans[(n, h, w)] = plan
         out = torch.empty(plan.out_shape, dtype=torch.uint8, device=self.device)
         return plan.run(x.contiguous(), out)

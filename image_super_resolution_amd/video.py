@@ -285,7 +285,7 @@ class FrameUpscaler:
         self.device = torch.device(device)
         self.batch, self.h, self.w = batch, height, width
         self.scale = 2 ** len(gw.scalers)
-        self.plan = engine.GeneratorPlan(gw, batch, height, width, self.device, True, True, mean, std)
+        self.plan = engine.make_plan(gw, batch, height, width, self.device, True, True, mean, std)
         H, W = height * self.scale, width * self.scale
         self.out_hw = (H, W)
         self.x_hwc = torch.zeros((batch, height, width, 3), dtype=torch.uint8, device=self.device)
