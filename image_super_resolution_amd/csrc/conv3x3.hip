@@ -40,6 +40,9 @@ struct C3 {
     static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol)
     // Ablation bits, timing-only builds (outputs wrong): 1 = no MFMA (operands
     // kept live), 2 = stage only chunk 0 (no refill), 4 = no epilogue stores.
+    // Experiment bits (outputs exact): 8/16 = blocks of the second dispatch round
+    // (blockIdx / 256 odd: the second block slot of each CU) start ~0.5/1 us late,
+    // so two co-resident blocks are out of phase (one's loads beside the other's MFMAs).
     static constexpr int ABL = ABL_;
     static constexpr int TH = R * WM;
     static constexpr int TW = 32;
@@ -236,6 +239,9 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     const int l31 = lane & 31;
     const int hh = lane >> 5;
     const int nchunks = C::CIN ? C::CIN / C::KC : d.cin / C::KC;
+    if constexpr (C::ABL & 24) {
+        if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_sleep((C::ABL & 8) ? 16 : 32);
+    }
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
     // x_sub2 (backward of PixelShuffle): halo pixel (row, col) of sub-position s
@@ -347,11 +353,38 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
                 }
 #pragma unroll
             for (int ia = 0; ia < NA; ++ia) {
+                if constexpr (C::ABL & 32) {
+                    // timing probe: dx > TLO fragments = previous dx's shifted one lane by DPP
+                    // (lanes 31/63 not fixed up: outputs wrong)
+                    if (st % TN != 0) {
+                        const int prev = C::PIPE ? set ^ 1 : set;
+                        auto* src = reinterpret_cast<int*>(&fa[prev][ia]);
+                        auto* dst = reinterpret_cast<int*>(&fa[set][ia]);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) dst[e] = __builtin_amdgcn_update_dpp(0, src[e], 0x130, 0xf, 0xf, false);
+                        continue;
+                    }
+                }
                 const int q = qw + (TLO + ia) * C::HC + dx;
                 fa[set][ia] = lds_read16(hp + halo_unit2(q, hh) * 16);
             }
         };
+        // one fragment of step st: idx < TN*NF â†’ weights (dyi, f), else activation row ia
+        auto read_one = [&](int st, int idx, int set) {
+            const int ks = st / TN, dx = TLO + st % TN;
+            if (idx < TN * NF) {
+                const int dyi = idx / NF, f = idx % NF;
+                const int n = f * 32 + l31;
+                const int u = ((ks * 9 + (TLO + dyi) * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
+                fb[set][dyi][f] = lds_read16(ws + u * 16);
+            } else {
+                const int ia = idx - TN * NF;
+                const int q = qw + (TLO + ia) * C::HC + dx;
+                fa[set][ia] = lds_read16(hs + ks * C::HIPL * 1024 + halo_unit2(q, hh) * 16);
+            }
+        };
         if constexpr (C::PIPE) load_step(0, 0);
+        if constexpr (C::PIPE == 2) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int st = 0; st < NS; ++st) {
             const int cur = C::PIPE ? (st & 1) : 0;
@@ -361,7 +394,31 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
                     stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST, st * C::IPW / C::SPL,
                           (st + 1) * C::IPW / C::SPL);
             }
-            if constexpr (C::PIPE) {
+            if constexpr (C::PIPE == 2) {
+                // interleaved: this step's MFMAs with the next step's fragment reads (one
+                // read after each MFMA), so at most one step's reads are in flight (<= 15,
+                // the lgkmcnt range: beyond it hipcc can only wait lgkmcnt(0))
+                constexpr int NRD = TN * NF + NA;  // reads per step
+                constexpr int NM = R * TN * NF;    // MFMAs per step
+                int m = 0;
+#pragma unroll
+                for (int ia = 0; ia < NA; ++ia)
+#pragma unroll
+                    for (int dyi = 0; dyi < TN; ++dyi) {
+                        const int r = ia - dyi;
+                        if (r >= 0 && r < R) {
+#pragma unroll
+                            for (int f = 0; f < NF; ++f) {
+                                acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
+                                if (st + 1 < NS)
+                                    for (int k = m * NRD / NM; k < (m + 1) * NRD / NM; ++k) read_one(st + 1, k, cur ^ 1);
+                                __builtin_amdgcn_sched_barrier(0);  // pin the (MFMA, reads) order
+                                ++m;
+                            }
+                        }
+                    }
+                continue;
+            } else if constexpr (C::PIPE) {
                 if (st + 1 < NS) load_step(st + 1, cur ^ 1);
                 // keep the prefetch ahead of this step's MFMAs (hipcc otherwise sinks
                 // each ds_read next to its first use and waits lgkmcnt(0) there)
@@ -380,6 +437,16 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
                         for (int f = 0; f < NF; ++f) {
                             if constexpr (C::ABL & 1) {
                                 asm volatile("" ::"v"(fa[cur][ia]), "v"(fb[cur][dyi][f]));
+                            } else if constexpr (C::ABL & 64) {
+                                // DVFS probe (outputs wrong): the same FLOPs as two 16x16x32 MFMAs
+                                f32x16& a = acc[r][f];
+                                const int h = (r + f) & 1;
+                                f32x4 c0 = {a[8 * h], a[8 * h + 1], a[8 * h + 2], a[8 * h + 3]};
+                                f32x4 c1 = {a[8 * h + 4], a[8 * h + 5], a[8 * h + 6], a[8 * h + 7]};
+                                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][dyi][f], fa[cur][ia], c0, 0, 0, 0);
+                                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][dyi][f], fa[cur][ia], c1, 0, 0, 0);
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) { a[8 * h + e] = c0[e]; a[8 * h + 4 + e] = c1[e]; }
                             } else {
                                 acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
                             }
@@ -446,7 +513,9 @@ static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
 // (tools/tune_conv.py on MI355X, N=16 128Â²: the 16x32-tile, 2-blocks/CU configs are
 // fastest on every shape of the generator; the 32x32 8-wave tiles win only at long K)
 // cout == 32 (RDB growth convs)
-using V_G0 = C3<4, 4, 1, 16, 2>; // 16x32, 4 waves, KC16 double buffer, 64 KB â†’ 2 blocks / CU
+// V_G0 / V_F0: the next step's fragment reads interleaved one per MFMA (PIPE 2): 2-7 % over the
+// batched prefetch, whose 18-24 reads in flight exceed lgkmcnt's range (so hipcc waited lgkmcnt(0))
+using V_G0 = C3<4, 4, 1, 16, 2, 0, 0, 2>; // 16x32, 4 waves, KC16 double buffer, 64 KB â†’ 2 blocks / CU
 using V_G1 = C3<4, 8, 1, 16, 3>; // 32x32 px tile, 8 waves, 3-deep KC16 ring
 using V_G2 = C3<2, 4, 1, 32, 2>; // 8x32, KC32, 2 blocks / CU
 using V_G3 = C3<2, 8, 1, 16, 3>; // 16x32, 8 waves x 2 rows, 3-deep KC16 ring
@@ -455,7 +524,7 @@ using V_W0 = C3<4, 4, 2, 16, 2>; // 16x32, 4 waves, KC16 double buffer, 80 KB â†
 using V_W1 = C3<4, 8, 2, 16, 2>; // 32x32 px tile, 8 waves, KC16 double buffer
 using V_W2 = C3<2, 4, 2, 32, 2>; // 8x32, KC32
 using V_W3 = C3<4, 4, 2, 32, 2>; // 16x32, KC32, 1 block / CU
-using V_F0 = C3<4, 4, 2, 16, 2, 192>; // RDB final conv 192â†’64: V_W0 with compile-time cin
+using V_F0 = C3<4, 4, 2, 16, 2, 192, 0, 2>; // RDB final conv 192â†’64: V_W0 with compile-time cin, PIPE 2
 
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
     if (d->cout % 64) {  // 32-cout tiles: growth convs (cout 32) and dgrad of them (96, 160)
@@ -475,6 +544,13 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 11: return launch3x3<C3<2, 4, 1, 16, 3>>(d, s);  // 8x32 tile, 3-deep ring (60 KB, 2 blocks/CU)
             case 12: return launch3x3<C3<4, 4, 1, 16, 3>>(d, s);  // 16x32 tile, 3-deep ring (1 block/CU)
             case 13: return launch3x3<C3<2, 4, 1, 16, 2>>(d, s);  // 8x32 tile, double buffer (3 blocks/CU)
+            case 14: return launch3x3<C3<4, 4, 1, 16, 2, 0, 8>>(d, s);   // V_G0, second block slot ~0.5 us late
+            case 15: return launch3x3<C3<4, 4, 1, 16, 2, 0, 16>>(d, s);  // V_G0, second block slot ~1 us late
+            case 16: return launch3x3<C3<4, 4, 1, 16, 2, 0, 32>>(d, s);  // probe: dx>0 activations by DPP shift
+            case 17: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // V_G0, reads interleaved with MFMAs
+            case 18: return launch3x3<C3<4, 4, 1, 32, 2, 0, 0, 2>>(d, s);  // KC32 (1 block/CU), interleaved
+            case 19: return launch3x3<C3<2, 4, 1, 32, 2, 0, 0, 2>>(d, s);  // 8x32 KC32, interleaved
+            case 20: return launch3x3<C3<4, 4, 1, 16, 2, 0, 64>>(d, s);  // DVFS probe: 2x 16x16x32 per 32x32x16
         }
         return -2;
     }
@@ -496,6 +572,18 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
                                       : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 1, 4, 1>>(d, s);
         case 11: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 1, 4, 2>>(d, s)  // both
                                       : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 1, 4, 2>>(d, s);
+        case 14: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 8>>(d, s)  // second block slot ~0.5 us late
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 8>>(d, s);
+        case 15: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 16>>(d, s)  // ~1 us late
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 16>>(d, s);
+        case 16: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 32>>(d, s)  // probe: DPP-shifted dx>0
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 32>>(d, s);
+        case 17: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 2>>(d, s)  // reads interleaved with MFMAs
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 2>>(d, s);
+        case 18: return d->cin == 192 ? launch3x3<C3<2, 4, 2, 32, 2, 192, 0, 2>>(d, s)  // 8x32 KC32, interleaved
+                                      : launch3x3<C3<2, 4, 2, 32, 2, 0, 0, 2>>(d, s);
+        case 20: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 64>>(d, s)  // DVFS probe (16x16x32)
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 64>>(d, s);
     }
     return -2;
 }
