@@ -124,6 +124,7 @@ SIGNATURES = {
     "isr_conv3x3_fwd_variant": (c_int32, [POINTER(IsrConvDesc), c_int32, c_void_p]),
     "isr_head9x9_fwd": (c_int32, [POINTER(IsrHeadDesc), c_void_p]),
     "isr_tail9x9_fwd": (c_int32, [POINTER(IsrTailDesc), c_void_p]),
+    "isr_tail9x9_fwd_variant": (c_int32, [POINTER(IsrTailDesc), c_int32, c_void_p]),
     "isr_mt_adam": (c_int32, [c_void_p, c_void_p, c_int32, POINTER(IsrAdamArgs), c_void_p, c_void_p]),
     "isr_mt_sumsq": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "isr_clip_coef": (c_int32, [c_void_p, c_int32, c_float, c_void_p, c_void_p]),

@@ -14,6 +14,7 @@ size_t conv3x3_packed_bytes(int cout, int cin);
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s);
 int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s);
+int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s);
 size_t head9x9_packed_bytes(int cout);
 size_t tail9x9_packed_bytes();
 int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
@@ -232,7 +233,7 @@ int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s) {
     return launched(isr::head9x9_fwd_dispatch(d, (hipStream_t)s), "head9x9");
 }
 
-int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s) {
+static int tail_validate(const isr_tail_desc* d) {
     if (!d) return fail(ISR_ERR_BAD_DESC, "tail9x9: null descriptor");
     if (d->n <= 0 || d->h <= 0 || d->w <= 0) return fail(ISR_ERR_BAD_DESC, "tail9x9: empty problem");
     if (d->ha % ISR_TILE_H || d->wa % ISR_TILE_W || d->ha < d->h || d->wa < d->w)
@@ -240,7 +241,21 @@ int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s) {
     if (d->cin != 64) return fail(ISR_ERR_UNSUPPORTED, "tail9x9: cin must be 64");
     if (!d->y || !d->wpack) return fail(ISR_ERR_BAD_DESC, "tail9x9: null output or weights");
     if (!view_ok(d->x, d->ha, d->wa, 4, 64, "tail9x9.x", 1)) return ISR_ERR_BAD_DESC;
+    return ISR_OK;
+}
+
+int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s) {
+    const int rc = tail_validate(d);
+    if (rc != ISR_OK) return rc;
     return launched(isr::tail9x9_fwd_dispatch(d, (hipStream_t)s), "tail9x9");
+}
+
+int isr_tail9x9_fwd_variant(const isr_tail_desc* d, int32_t variant, isr_stream_t s) {
+    const int rc = tail_validate(d);
+    if (rc != ISR_OK) return rc;
+    const int r = isr::tail9x9_fwd_variant(d, variant, (hipStream_t)s);
+    if (r == -2) return fail(ISR_ERR_UNSUPPORTED, "tail9x9: no variant %d", variant);
+    return launched(r, "tail9x9");
 }
 
 static int wgrad_validate(const isr_wgrad_desc* d) {

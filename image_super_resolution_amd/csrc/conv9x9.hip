@@ -268,6 +268,183 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
     }
 }
 
+// ---- persistent tail (variant 2, not production: see tail9x9_fwd_variant): one block per CU walks its tiles, 16-channel halo planes
+// stream through a 3-deep LDS ring (the next tile's first planes load while this
+// tile finishes), weights stay resident, and the ky-sum goes through small per-wave
+// partial-sum slices instead of a full T image.  Deterministic: each slice is
+// written by one wave in program order, the slices are added in a fixed order.
+namespace tailp {
+using tail::TH; using tail::TW; using tail::WM; using tail::TR; using tail::RT; using tail::HC; using tail::HIPL;
+constexpr int NST = 3;
+constexpr int GPW = 8;                          // glds per wave per plane (30 used + 2 dummy over 4 waves)
+constexpr int SLOT = GPW * WM * 1024;           // 32 KB
+constexpr int W_BYTES = tail::W_BYTES;          // 36 KB, 9 glds per wave
+constexpr int OS = 131;                         // floats per slice row (≡ 3 mod 64: the 27 (ky, co) lanes hit 27 banks)
+__host__ __device__ constexpr int lo(int w) { return 6 * w - 8 > 0 ? 6 * w - 8 : 0; }
+__host__ __device__ constexpr int hi(int w) { return 6 * w + 5 < TH - 1 ? 6 * w + 5 : TH - 1; }
+__host__ __device__ constexpr int rows_before(int w) { return w == 0 ? 0 : rows_before(w - 1) + hi(w - 1) - lo(w - 1) + 1; }
+constexpr int SLICE_ROWS = rows_before(WM);
+constexpr int SLICE_BYTES = SLICE_ROWS * OS * 4;
+constexpr int LDS = W_BYTES + NST * SLOT + SLICE_BYTES;
+static_assert(LDS <= 163840, "LDS budget");
+static_assert(HIPL <= GPW * WM && tail::W_INSTR % WM == 0, "");
+static_assert(RT * WM == TR && TH * TW % 256 == 0, "");
+}  // namespace tailp
+
+// ABL (timing probes, outputs wrong): 1 = plain LDS stores instead of ds_add, 2 = no MFMAs,
+// 4 = no epilogue (slices / stores)
+template <int ABL = 0>
+__global__ __launch_bounds__(256, 1) void tail9x9_pkernel(isr_tail_desc d, int ntiles) {
+    using namespace tailp;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* wl = smem;
+    char* ring = smem + W_BYTES;
+    float* slices = reinterpret_cast<float*>(smem + W_BYTES + NST * SLOT);
+    const int wave = wave_id();
+    const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+    const int G = gridDim.x;
+    const int b = xcd_remap(blockIdx.x, G);
+    const int mine = b < ntiles ? (ntiles - b + G - 1) / G : 0;
+    const int nch = mine * 4;
+    const int nbx = d.wa / TW, nby = d.ha / TH;
+    const size_t pstride = plane_bytes(d.x);
+    const int xrow = d.x.wp * 32;
+
+    for (int j = wave; j < tail::W_INSTR; j += WM)
+        glds16((const char*)d.wpack + j * 1024 + lane * 16, wl + j * 1024);
+    for (int i = threadIdx.x; i < SLICE_ROWS * OS; i += 256) slices[i] = 0.f;
+
+    uint32_t off[GPW];
+#pragma unroll
+    for (int k = 0; k < GPW; ++k) {
+        const int j = wave + WM * k;
+        uint32_t o = 0;  // j >= HIPL: dummy copy into the slot's unused tail
+        if (j < HIPL) {
+            const int u = j * 64 + lane;
+            const int q = u >> 1;
+            const int row = q / HC, col = q - row * HC;
+            const int c = (u & 1) ^ ((q >> 3) & 1);
+            o = (uint32_t)(row * xrow + col * 32 + c * 16);
+        }
+        off[k] = o;
+    }
+    auto tile_of = [&](int g, int& img, int& y0, int& x0) {
+        int t = b + (g >> 2) * G;
+        x0 = (t % nbx) * TW; t /= nbx;
+        y0 = (t % nby) * TH;
+        img = t / nby;
+    };
+    auto issue = [&](int g) {
+        int img, y0, x0;
+        tile_of(g, img, y0, x0);
+        const char* base = view_at(d.x, img, y0 - 4, x0 - 4, 0) + (size_t)(g & 3) * pstride;
+        char* dst = ring + (g % NST) * SLOT;
+#pragma unroll
+        for (int k = 0; k < GPW; ++k) glds16(base + off[k], dst + (wave + WM * k) * 1024);
+    };
+    if (nch > 0) issue(0);
+    if (nch > 1) issue(1);
+
+    f32x16 acc[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
+    const int n = l31, ky = n / 3, co = n - 3 * (n / 3);
+    float* myslice = slices + rows_before(wave) * OS;  // wave-uniform
+    const int mylo = lo(wave), myhi = hi(wave);
+
+    for (int g = 0; g < nch; ++g) {
+        if (g + 1 < nch) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
+        } else {
+            wait_vm0();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (g + 2 < nch) issue(g + 2);
+
+        const char* hs = ring + (g % NST) * SLOT;
+        const int c16 = g & 3, chunk = c16 >> 1, ks = c16 & 1;
+        bf16x8 fb[2], fa[2][RT];
+        auto rd = [&](int kx, int idx, int set) {
+            if (idx == 0) {
+                fb[set] = lds_read16(wl + ((((kx * 2 + chunk) * 2 + ks) * 32 + n) * 2 + (hh ^ ((n >> 3) & 1))) * 16);
+            } else {
+                const int t = idx - 1;
+                fa[set][t] = lds_read16(hs + halo_unit2((wave * RT + t) * HC + kx + l31, hh) * 16);
+            }
+        };
+#pragma unroll
+        for (int i = 0; i <= RT; ++i) rd(0, i, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kx = 0; kx < 9; ++kx) {
+            const int cur = kx & 1;
+#pragma unroll
+            for (int t = 0; t < RT; ++t) {
+                if constexpr (ABL & 2) {
+                    asm volatile("" ::"v"(fa[cur][t]), "v"(fb[cur]));
+                } else {
+                    acc[t] = mfma32(fa[cur][t], fb[cur], acc[t]);
+                }
+                if (kx + 1 < 9)
+                    for (int i = t * (RT + 1) / RT; i < (t + 1) * (RT + 1) / RT; ++i) rd(kx + 1, i, cur ^ 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+
+        if (c16 == 3 && !(ABL & 4)) {  // tile done: partial ky-sums → this wave's slice, then reduce + tanh + store
+#pragma unroll
+            for (int t = 0; t < RT; ++t) {
+                const int y = wave * RT + t - ky;
+                const bool ok = n < 27 && y >= mylo && y <= myhi;
+#pragma unroll
+                for (int gg = 0; gg < 16; ++gg) {
+                    const int px = (gg & 3) + 8 * (gg >> 2) + 4 * hh;
+                    if constexpr (ABL & 1) {
+                        if (ok) myslice[(y - mylo) * OS + px * 3 + co] = acc[t][gg];
+                    } else {
+                        if (ok) atomicAdd(&myslice[(y - mylo) * OS + px * 3 + co], acc[t][gg]);
+                    }
+                    acc[t][gg] = 0.f;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            int img, y0, x0;
+            tile_of(g, img, y0, x0);
+            const size_t plane = (size_t)d.h * d.w;
+#pragma unroll
+            for (int k = 0; k < 3 * TH * TW / 256; ++k) {
+                const int it = threadIdx.x + 256 * k;
+                const int oc = it / (TH * TW), rem = it - oc * (TH * TW);
+                const int y = rem / TW, px = rem - y * TW;
+                float s = d.bias ? d.bias[oc] : 0.f;
+#pragma unroll
+                for (int w = 0; w < WM; ++w) {
+                    if (y >= lo(w) && y <= hi(w)) {
+                        float* p = slices + (rows_before(w) + y - lo(w)) * OS + px * 3 + oc;
+                        s += *p;
+                        *p = 0.f;
+                    }
+                }
+                const int yy = y0 + y, xx = x0 + px;
+                if (yy < d.h && xx < d.w) {
+                    const size_t o = (size_t)img * 3 * plane + (size_t)oc * plane + (size_t)yy * d.w + xx;
+                    const float th = tanhf(s);
+                    if (d.y_u8) {
+                        const float q = rintf((th + 1.f) / 2.f * 255.f);
+                        ((uint8_t*)d.y)[o] = (uint8_t)fminf(fmaxf(q, 0.f), 255.f);
+                    } else {
+                        ((float*)d.y)[o] = th;
+                    }
+                }
+            }
+        }
+    }
+}
+
 __global__ void pack_tail_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
     const int total = tail::W_BYTES / 2;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
@@ -299,7 +476,39 @@ int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s) {
+int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
+    // production = variant 1, the one-tile-per-block kernel: the persistent kernel's main
+    // loop streams at ~5 TB/s, but its partial-sum epilogue (LDS atomics: 990 us; plain
+    // stores: 440 us vs 370 us for the whole per-tile kernel, tools/tune_tail.py) loses
+    if (variant == 0) variant = 1;
+    if (variant == 2 || (variant >= 10 && variant <= 17)) {  // persistent
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                cus = 256;
+        }
+        const int ntiles = d->n * (d->ha / tail::TH) * (d->wa / tail::TW);
+        const int grid = ntiles < cus ? ntiles : cus;
+        auto go = [&](auto kern) {
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, tailp::LDS);
+                attr = true;
+            }
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), tailp::LDS, s, *d, ntiles);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        };
+        switch (variant) {
+            case 11: return go(tail9x9_pkernel<1>);
+            case 12: return go(tail9x9_pkernel<2>);
+            case 14: return go(tail9x9_pkernel<4>);
+            case 16: return go(tail9x9_pkernel<6>);
+            default: return go(tail9x9_pkernel<0>);
+        }
+    }
+    if (variant != 1) return -2;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)tail9x9_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, tail::LDS);
@@ -309,6 +518,8 @@ int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s) {
     hipLaunchKernelGGL(tail9x9_kernel, grid, dim3(256), tail::LDS, s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s) { return tail9x9_fwd_variant(d, 0, s); }
 
 size_t head9x9_packed_bytes(int cout) { return (size_t)9 * 3 * cout * 16 * 2; }
 size_t tail9x9_packed_bytes() { return tail::W_BYTES; }

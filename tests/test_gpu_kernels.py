@@ -164,6 +164,35 @@ def test_tail9x9(u8):
         close(out, ref, tol=5e-3, mean_tol=5e-4)
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 40, 72), (5, 128, 160)])
+def test_tail9x9_persistent_vs_per_tile(n, h, w):
+    """Persistent tail variant (one block per CU; (5, 128, 160) has 400 tiles, so blocks
+    walk several) vs the production one-tile-per-block kernel, and run-to-run bit equality."""
+    import ctypes
+    from image_super_resolution_amd import ops, _lib
+    lib = _lib.load()
+    x = _mk(n, 64, h, w, 21) * 0.5
+    W = _w(3, 64, 9, 22)
+    b = torch.randn(3, device=DEV) * 0.1
+    xb = ops.ActBuffer.from_nchw(x, pad=4)
+    wp = ops.pack_tail9x9(W)
+    outs = {}
+    for dt in (torch.float32, torch.uint8):
+        for v in (1, 2, 2):
+            o = torch.empty(n, 3, h, w, device=DEV, dtype=dt)
+            d = ops.tail9x9_desc(xb, wp, b, o)
+            ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(d), v, ops._stream()), "tail variant")
+            torch.cuda.synchronize()
+            outs.setdefault((dt, v), []).append(o)
+        a, p0, p1 = outs[(dt, 1)][0], outs[(dt, 2)][0], outs[(dt, 2)][1]
+        assert torch.equal(p0, p1)
+        if dt == torch.float32:
+            assert (a - p0).abs().max().item() < 1e-5
+        else:
+            dd = (a.float() - p0.float()).abs()
+            assert dd.max().item() <= 1 and (dd > 0).float().mean().item() < 1e-3
+
+
 def test_bad_descriptor_raises():
     from image_super_resolution_amd import ops, _lib
     x = ops.ActBuffer.alloc(1, 16, 32, 48, 1, DEV)
