@@ -520,7 +520,7 @@ using V_G1 = C3<4, 8, 1, 16, 3>; // 32x32 px tile, 8 waves, 3-deep KC16 ring
 using V_G2 = C3<2, 4, 1, 32, 2>; // 8x32, KC32, 2 blocks / CU
 using V_G3 = C3<2, 8, 1, 16, 3>; // 16x32, 8 waves x 2 rows, 3-deep KC16 ring
 // cout % 64 == 0
-using V_W0 = C3<4, 4, 2, 16, 2>; // 16x32, 4 waves, KC16 double buffer, 80 KB → 2 blocks / CU
+using V_W0 = C3<4, 4, 2, 16, 2, 0, 0, 2>; // 16x32, 4 waves, KC16 double buffer, 80 KB → 2 blocks / CU, PIPE 2
 using V_W1 = C3<4, 8, 2, 16, 2>; // 32x32 px tile, 8 waves, KC16 double buffer
 using V_W2 = C3<2, 4, 2, 32, 2>; // 8x32, KC32
 using V_W3 = C3<4, 4, 2, 32, 2>; // 16x32, KC32, 1 block / CU

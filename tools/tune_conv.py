@@ -38,7 +38,9 @@ def main():
     shapes = [(64, 32, 1, hw), (96, 32, 1, hw), (128, 32, 1, hw), (160, 32, 1, hw), (192, 64, 1, hw),
               (64, 64, 1, hw), (64, 256, 2, hw), (64, 256, 2, 2 * hw),
               # long-K shapes: fixed per-block latency amortised → main-loop throughput
-              (512, 32, 1, hw), (512, 64, 1, hw)]
+              (512, 32, 1, hw), (512, 64, 1, hw),
+              # backward (dgrad) shapes of the growth convs: cin' = 32, cout' = layer cin
+              (32, 64, 1, hw), (32, 96, 1, hw), (32, 128, 1, hw), (32, 160, 1, hw)]
     if args.only:
         keep = {tuple(int(v) for v in s.split("x")) for s in args.only.split(",")}
         shapes = [s for s in shapes if (s[0], s[1]) in keep]
