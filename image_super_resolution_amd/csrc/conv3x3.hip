@@ -551,6 +551,9 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 18: return launch3x3<C3<4, 4, 1, 32, 2, 0, 0, 2>>(d, s);  // KC32 (1 block/CU), interleaved
             case 19: return launch3x3<C3<2, 4, 1, 32, 2, 0, 0, 2>>(d, s);  // 8x32 KC32, interleaved
             case 20: return launch3x3<C3<4, 4, 1, 16, 2, 0, 64>>(d, s);  // DVFS probe: 2x 16x16x32 per 32x32x16
+            case 21: return launch3x3<C3<8, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // 32x32 tile, 8 rows per wave (1 block/CU)
+            case 22: return launch3x3<C3<8, 2, 1, 16, 2, 0, 0, 2>>(d, s);  // 16x32 tile, 2 waves x 8 rows
+            case 23: return launch3x3<C3<2, 8, 1, 16, 2, 0, 0, 2>>(d, s);  // 16x32 tile, 8 waves x 2 rows
         }
         return -2;
     }
