@@ -291,8 +291,8 @@ static_assert(HIPL <= GPW * WM && tail::W_INSTR % WM == 0, "");
 static_assert(RT * WM == TR && TH * TW % 256 == 0, "");
 }  // namespace tailp
 
-// ABL (timing probes, outputs wrong): 1 = plain LDS stores instead of ds_add, 2 = no MFMAs,
-// 4 = no epilogue (slices / stores)
+// ABL (timing probes, outputs wrong): 2 = no MFMAs, 4 = no epilogue (slices / stores),
+// 8 = slices but no reduce / store
 template <int ABL = 0>
 __global__ __launch_bounds__(256, 1) void tail9x9_pkernel(isr_tail_desc d, int ntiles) {
     using namespace tailp;
@@ -354,6 +354,41 @@ __global__ __launch_bounds__(256, 1) void tail9x9_pkernel(isr_tail_desc d, int n
     float* myslice = slices + rows_before(wave) * OS;  // wave-uniform
     const int mylo = lo(wave), myhi = hi(wave);
 
+    // reduce the 4 wave slices of the tile ending at chunk g (fixed order: deterministic),
+    // zero them for the next tile, bias + tanh (+ uint8), store NCHW
+    auto finish = [&](int g) {
+        if constexpr (ABL & 8) return;
+        int img, y0, x0;
+        tile_of(g, img, y0, x0);
+        const size_t plane = (size_t)d.h * d.w;
+#pragma unroll
+        for (int k = 0; k < 3 * TH * TW / 256; ++k) {
+            const int it = threadIdx.x + 256 * k;
+            const int oc = it / (TH * TW), rem = it - oc * (TH * TW);
+            const int y = rem / TW, px = rem - y * TW;
+            float s = d.bias ? d.bias[oc] : 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) {
+                if (y >= lo(w) && y <= hi(w)) {
+                    float* p = slices + (rows_before(w) + y - lo(w)) * OS + px * 3 + oc;
+                    s += *p;
+                    *p = 0.f;
+                }
+            }
+            const int yy = y0 + y, xx = x0 + px;
+            if (yy < d.h && xx < d.w) {
+                const size_t o = (size_t)img * 3 * plane + (size_t)oc * plane + (size_t)yy * d.w + xx;
+                const float th = tanhf(s);
+                if (d.y_u8) {
+                    const float q = rintf((th + 1.f) / 2.f * 255.f);
+                    ((uint8_t*)d.y)[o] = (uint8_t)fminf(fmaxf(q, 0.f), 255.f);
+                } else {
+                    ((float*)d.y)[o] = th;
+                }
+            }
+        }
+    };
+
     for (int g = 0; g < nch; ++g) {
         if (g + 1 < nch) {
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
@@ -362,6 +397,10 @@ __global__ __launch_bounds__(256, 1) void tail9x9_pkernel(isr_tail_desc d, int n
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        if (!(ABL & 4) && g > 0 && (g & 3) == 0) {
+            finish(g - 1);  // slices complete: every wave passed this barrier after writing them
+            // the slices are re-zeroed here and next written after 3 more chunk barriers
+        }
         if (g + 2 < nch) issue(g + 2);
 
         const char* hs = ring + (g % NST) * SLOT;
@@ -394,54 +433,36 @@ __global__ __launch_bounds__(256, 1) void tail9x9_pkernel(isr_tail_desc d, int n
             }
         }
 
-        if (c16 == 3 && !(ABL & 4)) {  // tile done: partial ky-sums → this wave's slice, then reduce + tanh + store
+        if (c16 == 3 && !(ABL & 4)) {  // tile done: partial ky-sums → this wave's slice
+            // read-modify-write in program order (LDS is in order per wave; within one
+            // instruction the 27 (ky, co) lanes hit distinct rows, so no atomics are needed)
 #pragma unroll
             for (int t = 0; t < RT; ++t) {
                 const int y = wave * RT + t - ky;
                 const bool ok = n < 27 && y >= mylo && y <= myhi;
+                float* row = myslice + (y - mylo) * OS + co;
+                float v[16];
 #pragma unroll
                 for (int gg = 0; gg < 16; ++gg) {
                     const int px = (gg & 3) + 8 * (gg >> 2) + 4 * hh;
-                    if constexpr (ABL & 1) {
-                        if (ok) myslice[(y - mylo) * OS + px * 3 + co] = acc[t][gg];
-                    } else {
-                        if (ok) atomicAdd(&myslice[(y - mylo) * OS + px * 3 + co], acc[t][gg]);
-                    }
+                    v[gg] = ok ? row[px * 3] : 0.f;
+                }
+#pragma unroll
+                for (int gg = 0; gg < 16; ++gg) {
+                    const int px = (gg & 3) + 8 * (gg >> 2) + 4 * hh;
+                    if (ok) row[px * 3] = v[gg] + acc[t][gg];
                     acc[t][gg] = 0.f;
                 }
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            int img, y0, x0;
-            tile_of(g, img, y0, x0);
-            const size_t plane = (size_t)d.h * d.w;
-#pragma unroll
-            for (int k = 0; k < 3 * TH * TW / 256; ++k) {
-                const int it = threadIdx.x + 256 * k;
-                const int oc = it / (TH * TW), rem = it - oc * (TH * TW);
-                const int y = rem / TW, px = rem - y * TW;
-                float s = d.bias ? d.bias[oc] : 0.f;
-#pragma unroll
-                for (int w = 0; w < WM; ++w) {
-                    if (y >= lo(w) && y <= hi(w)) {
-                        float* p = slices + (rows_before(w) + y - lo(w)) * OS + px * 3 + oc;
-                        s += *p;
-                        *p = 0.f;
-                    }
-                }
-                const int yy = y0 + y, xx = x0 + px;
-                if (yy < d.h && xx < d.w) {
-                    const size_t o = (size_t)img * 3 * plane + (size_t)oc * plane + (size_t)yy * d.w + xx;
-                    const float th = tanhf(s);
-                    if (d.y_u8) {
-                        const float q = rintf((th + 1.f) / 2.f * 255.f);
-                        ((uint8_t*)d.y)[o] = (uint8_t)fminf(fmaxf(q, 0.f), 255.f);
-                    } else {
-                        ((float*)d.y)[o] = th;
-                    }
-                }
-            }
         }
+    }
+    // the last tile's reduce + store (earlier tiles' run at the top of the next tile's
+    // first chunk, before that chunk's refill is issued, so the refill stays the youngest
+    // vmcnt group and the next wait stays exact)
+    if (nch > 0 && !(ABL & 4)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        finish(nch - 1);
     }
 }
 
@@ -477,9 +498,9 @@ int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s) {
 }
 
 int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
-    // production = variant 1, the one-tile-per-block kernel: the persistent kernel's main
-    // loop streams at ~5 TB/s, but its partial-sum epilogue (LDS atomics: 990 us; plain
-    // stores: 440 us vs 370 us for the whole per-tile kernel, tools/tune_tail.py) loses
+    // production = variant 1, the one-tile-per-block kernel (≈375 us at 16 x 512²): the
+    // persistent variant 2 measures 515 us (LDS-atomic slices: 990 us; its main loop alone
+    // ≈330 us at one wave per SIMD; tools/tune_tail.py)
     if (variant == 0) variant = 1;
     if (variant == 2 || (variant >= 10 && variant <= 17)) {  // persistent
         static int cus = 0;
@@ -501,10 +522,8 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             return hipGetLastError() == hipSuccess ? 0 : -1;
         };
         switch (variant) {
-            case 11: return go(tail9x9_pkernel<1>);
             case 12: return go(tail9x9_pkernel<2>);
-            case 14: return go(tail9x9_pkernel<4>);
-            case 16: return go(tail9x9_pkernel<6>);
+            case 13: return go(tail9x9_pkernel<8>);
             default: return go(tail9x9_pkernel<0>);
         }
     }
