@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--round", default="r01")
+    ap.add_argument("--backend", default="nccl", help="process-group backend for N>1 (nccl = RCCL)")
     ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams the batch is split over (default engine.DEFAULT_STREAMS)")
     return ap.parse_args()
@@ -89,10 +90,16 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    # one process per GPU; local % device_count only matters for a rehearsal with more
+    # ranks than GPUs (tools/rehearse_multi.sh on a 1-GPU box, --backend gloo)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL
+        else:
+            dist.init_process_group(args.backend)
 
     from image_super_resolution_amd import engine, models, ops
     from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_state_dict
@@ -133,7 +140,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
 
