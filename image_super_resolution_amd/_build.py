@@ -42,8 +42,13 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     objdir.mkdir(exist_ok=True)
     LIBDIR.mkdir(exist_ok=True)
 
+    headers = list(CSRC.glob("*.h")) + [ROOT / "include" / "isr.h", Path(__file__)]
+    newest_header = max(p.stat().st_mtime for p in headers)
+
     def compile_one(src: Path) -> Path:
         obj = objdir / (src.stem + ".o")
+        if not force and obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, newest_header):
+            return obj  # incremental: object newer than its source and every header
         cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

@@ -22,6 +22,7 @@ int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale, int sub2, hipStream_t s);
 int conv3x3_pack_batch(const isr_pack_item* items, int n, hipStream_t s);
 int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s);
+int pixel_shuffle2_dispatch(const isr_ew_desc* d, hipStream_t s);
 int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s);
 int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s);
 int blocked_to_nchw_dispatch(const isr_convert_desc* d, hipStream_t s);
@@ -348,6 +349,21 @@ int isr_ew_combine(const isr_ew_desc* d, isr_stream_t s) {
     if (d->b.data && !view_ok(d->b, d->ha, d->wa, 0, d->c, "ew.b", 1)) return ISR_ERR_BAD_DESC;
     if (d->m.data && !view_ok(d->m, d->ha, d->wa, 0, d->c, "ew.m", 1)) return ISR_ERR_BAD_DESC;
     return launched(isr::ew_combine_dispatch(d, (hipStream_t)s), "ew_combine");
+}
+
+int isr_pixel_shuffle2(const isr_ew_desc* d, isr_stream_t s) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "pixel_shuffle2: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0 || d->c % 16)
+        return fail(ISR_ERR_BAD_DESC, "pixel_shuffle2: bad problem n=%d h=%d w=%d c=%d", d->n, d->h, d->w, d->c);
+    if (d->h % 2 || d->w % 2) return fail(ISR_ERR_BAD_DESC, "pixel_shuffle2: output %dx%d must be even", d->h, d->w);
+    if (d->ha < d->h || d->wa < d->w || d->ha % 2 || d->wa % 2)
+        return fail(ISR_ERR_BAD_DESC, "pixel_shuffle2: computed region %dx%d must be even and cover %dx%d", d->ha, d->wa,
+                    d->h, d->w);
+    if (d->b.data || d->m.data) return fail(ISR_ERR_UNSUPPORTED, "pixel_shuffle2: takes no b / m operand");
+    if (!view_ok(d->y, d->ha, d->wa, 0, d->c, "pixel_shuffle2.y", 1) ||
+        !view_ok(d->a, d->ha / 2, d->wa / 2, 0, 4 * d->c, "pixel_shuffle2.a", 1))
+        return ISR_ERR_BAD_DESC;
+    return launched(isr::pixel_shuffle2_dispatch(d, (hipStream_t)s), "pixel_shuffle2");
 }
 
 static int convert_validate(const isr_convert_desc* d, const char* who) {

@@ -46,6 +46,45 @@ int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// PixelShuffle(2) + LeakyReLU between channel-blocked views (isr_pixel_shuffle2):
+// y[c] at (y, x) = act(sa * a[4c + 2(y&1) + (x&1)] at (y/2, x/2)).  One thread per
+// (output pixel, 8 output channels): the 8 source channels 4c+s .. 4c+28+s are
+// gathered from the 32 channels (two 16-channel planes) at the source pixel; the
+// four sub-pixel threads of a source pixel re-read the same 64 bytes from L2.
+__global__ __launch_bounds__(256) void pixel_shuffle2_kernel(isr_ew_desc d) {
+    const int cg = d.c / 8;
+    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        size_t r = i;
+        const int half = r % 2; r /= 2;
+        const int x = r % d.wa; r /= d.wa;
+        const int y = r % d.ha; r /= d.ha;
+        const int pl = r % (d.c / 16);
+        const int img = (int)(r / (d.c / 16));
+        const int c = pl * 16 + half * 8;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (y < d.h && x < d.w) {
+            const int s = 2 * (y & 1) + (x & 1);
+            float t[32];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) load8_bf16(view_at(d.a, img, y >> 1, x >> 1, 4 * c + 8 * q), t + 8 * q);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float u = t[4 * k + s] * d.sa;
+                v[k] = u > 0.f ? u : u * d.mslope;
+            }
+        }
+        store8_bf16(view_at(d.y, img, y, x, c), v);
+    }
+}
+
+int pixel_shuffle2_dispatch(const isr_ew_desc* d, hipStream_t s) {
+    const size_t total = (size_t)d->n * d->ha * d->wa * (d->c / 8);
+    const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    hipLaunchKernelGGL(pixel_shuffle2_kernel, dim3(blocks), dim3(256), 0, s, *d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 }  // namespace isr
 
 namespace isr {

@@ -275,6 +275,69 @@ class SRGAN(nn.Module):
         return self.res_net(inputs)
 
 
+class ResidualBlock1(nn.Module):
+    """x + Conv(act=False)(Conv(act)(x)), both convs with BN (utils/models.py:202-209)."""
+
+    def __init__(self, in_channel, out_channel, hidden_channel, kernel, act):
+        super().__init__()
+        self.m = nn.Sequential(Conv(in_channel, hidden_channel, kernel, 1, None, act=act),
+                               Conv(hidden_channel, out_channel, kernel, 1, None, act=False))
+
+    def forward(self, inputs):
+        _require_cuda(inputs, "ResidualBlock1")
+        _no_train(self, "ResidualBlock1")
+        c0, c1 = self.m[0].conv, self.m[1].conv
+        if c0.kernel_size != (3, 3) or c1.kernel_size != (3, 3) or c1.out_channels != c0.in_channels:
+            raise NotImplementedError("HIP ResidualBlock1 covers 3x3 blocks with out_channel == in_channel")
+        p0 = engine._pack3(_conv_sd(self.m[0]), "x", inputs.device)
+        p1 = engine._pack3(_conv_sd(self.m[1]), "x", inputs.device)
+        xb = ActBuffer.from_nchw(inputs.float(), pad=1)
+        hb = ActBuffer.alloc(xb.n, xb.h, xb.w, p0.cout, 1, inputs.device)
+        yb = ActBuffer.alloc(xb.n, xb.h, xb.w, p1.cout, 1, inputs.device)
+        ops.conv3x3(xb, p0.cin, p0.w, p0.b, p0.cout, hb, slope=_slope(self.m[0].act))
+        ops.conv3x3(hb, p1.cin, p1.w, p1.b, p1.cout, yb, slope=1.0, r1=xb, s1=1.0)
+        return yb.to_nchw()
+
+
+class Denoise(nn.Module):
+    """Same-resolution denoiser (utils/models.py:672-706), trained by
+    `train.py --train_denoise` (train.py:204-205).  Inference runs on libisr
+    (denoise.py); input height / width must be even, as in the reference."""
+
+    def __init__(self, residual_blocks):
+        super().__init__()
+        act = nn.LeakyReLU(0.2)
+        self.conv0 = nn.Sequential(ConvWithoutBN(3, 64, 9, 1, act=act))
+        self.residual_0 = nn.Sequential(*[ResidualBlock1(64, 64, 64, 3, act=act)
+                                          for _ in range(residual_blocks // 2)])
+        self.residual_conv0 = ConvWithoutBN(64, 256, 3, 2, act=act)
+        self.residual_1 = nn.Sequential(*[ResidualBlock1(256, 256, 256, 3, act) for _ in range(2)])
+        self.residual_conv1 = nn.Sequential(nn.PixelShuffle(2), nn.LeakyReLU(0.2))
+        self.residual_2 = nn.Sequential(*[ResidualBlock1(64, 64, 64, 3, act=act)
+                                          for _ in range(residual_blocks // 2)])
+        self.conv1 = Conv(64, 64, 3, 1, None, act=False)
+        self.conv2 = nn.Sequential(ConvWithoutBN(64, 3, 9, 1, None, act=nn.Tanh()))
+        for x in self.modules():
+            if hasattr(x, "inplace"):
+                x.inplace = True
+
+    def _packed(self, device):
+        from .denoise import pack_denoise
+        key = (str(device),) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
+        cache = self.__dict__.get("_isr_pack")
+        if cache is None or cache[0] != key:
+            dw = pack_denoise(self.state_dict(), device=device)
+            self.__dict__["_isr_pack"] = (key, dw)
+            return dw
+        return cache[1]
+
+    def forward(self, inputs: torch.Tensor) -> torch.Tensor:
+        _require_cuda(inputs, "Denoise")
+        _no_train(self, "Denoise")
+        from .denoise import run_denoise
+        return run_denoise(self._packed(inputs.device), inputs)
+
+
 def fuse_conv_and_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
     """utils/models.py:366-406 — returns a biased Conv2d with BN folded in."""
     fused = nn.Conv2d(conv.in_channels, conv.out_channels, kernel_size=conv.kernel_size, stride=conv.stride,

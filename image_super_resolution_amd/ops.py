@@ -407,6 +407,20 @@ def ew_combine(y: ActBuffer, a: ActBuffer, c: int, **kw) -> None:
     check(_lib.load().isr_ew_combine(ctypes.byref(ew_combine_desc(y, a, c, **kw)), _stream()), "isr_ew_combine")
 
 
+def pixel_shuffle2_desc(y: ActBuffer, a: ActBuffer, c: int, *, slope: float = 1.0, sa: float = 1.0) -> IsrEwDesc:
+    """y[0:c] (grid 2h x 2w) = LeakyReLU_slope(sa * PixelShuffle(2)(a[0:4c]))."""
+    d = IsrEwDesc()
+    d.n, d.h, d.w, d.ha, d.wa, d.c = y.n, y.h, y.w, y.ha, y.wa, c
+    d.y, d.a, d.b, d.m = y.view(0), a.view(0), _NULL_VIEW, _NULL_VIEW
+    d.sa, d.sb, d.mslope = sa, 0.0, slope
+    return d
+
+
+def pixel_shuffle2(y: ActBuffer, a: ActBuffer, c: int, **kw) -> None:
+    check(_lib.load().isr_pixel_shuffle2(ctypes.byref(pixel_shuffle2_desc(y, a, c, **kw)), _stream()),
+          "isr_pixel_shuffle2")
+
+
 def convert_desc(nchw: torch.Tensor, v: ActBuffer, *, v_coff: int = 0, scale: torch.Tensor | None = None,
                  shift: torch.Tensor | None = None, m: ActBuffer | None = None, mslope: float = 1.0,
                  m_coff: int = 0) -> IsrConvertDesc:

@@ -195,6 +195,15 @@ typedef struct isr_ew_desc {
 } isr_ew_desc;
 int isr_ew_combine(const isr_ew_desc* d, isr_stream_t s);
 
+/* PixelShuffle(2) + LeakyReLU(mslope) between channel-blocked views (same descriptor):
+ *   y[c] at (y, x) = act(sa * a[4c + 2*(y%2) + (x%2)] at (y/2, x/2)),  c < d->c
+ * (n, h, w, ha, wa) is the OUTPUT grid (even); a holds 4c channels on the
+ * (h/2) x (w/2) grid; b and m must be NULL.  Zeros outside the valid region.
+ * Replaces: Denoise.residual_conv1 = Sequential(PixelShuffle(2), LeakyReLU(0.2))
+ * (utils/models.py:687) applied to the output of a ResidualBlock1 (:202-209),
+ * whose residual add precedes the shuffle so it cannot ride a conv epilogue. */
+int isr_pixel_shuffle2(const isr_ew_desc* d, isr_stream_t s);
+
 /* Layout conversion between NCHW fp32 tensors and channel-blocked views
  * (network / loss boundaries: the VGG19 input, utils/loss.py:16-24, and the
  * gradient it receives).  to_blocked writes channels [0, round16(c)) of v (zeros

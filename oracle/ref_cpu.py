@@ -87,6 +87,35 @@ def generator(sd: dict, x: torch.Tensor, *, num_blocks: int, scale: int, enchant
     return torch.tanh(F.conv2d(y, w, sd[f"{p}conv2.conv.bias"], padding=w.shape[-1] // 2))
 
 
+def residual_block1(sd: dict, prefix: str, x: torch.Tensor, slope: float = 0.2) -> torch.Tensor:
+    """ResidualBlock1.forward (utils/models.py:202-209): x + Conv(act=False)(Conv(act)(x))."""
+    h = conv_unit(sd, f"{prefix}.m.0", x, slope)
+    return x + conv_unit(sd, f"{prefix}.m.1", h, None)
+
+
+def denoise(sd: dict, x: torch.Tensor) -> torch.Tensor:
+    """Denoise.forward (utils/models.py:695-706); every act is LeakyReLU(0.2) (:676-690).
+
+    conv0 9x9 → residual_0 → residual_conv0 (3x3 stride 2, pad 1, +bias, act)
+    → residual_1 (256 ch) → PixelShuffle(2) + act → residual_2 → conv1 + trunk → conv2 9x9 + tanh."""
+    def chain(name, y):
+        n = len({int(k[len(name) + 1:].split(".")[0]) for k in sd if k.startswith(name + ".")})
+        for i in range(n):
+            y = residual_block1(sd, f"{name}.{i}", y)
+        return y
+
+    feat = conv_unit(sd, "conv0.0", x, 0.2)
+    r = chain("residual_0", feat)
+    r = F.leaky_relu(F.conv2d(r, sd["residual_conv0.conv.weight"], sd["residual_conv0.conv.bias"], stride=2,
+                              padding=1), 0.2)
+    r = chain("residual_1", r)
+    r = F.leaky_relu(F.pixel_shuffle(r, 2), 0.2)
+    r = chain("residual_2", r)
+    y = feat + conv_unit(sd, "conv1", r, None)
+    w = sd["conv2.0.conv.weight"]
+    return torch.tanh(F.conv2d(y, w, sd["conv2.0.conv.bias"], padding=w.shape[-1] // 2))
+
+
 def count_blocks(sd: dict, prefix: str = "") -> int:
     p = f"{prefix}." if prefix else ""
     idx = {int(k[len(p) + len("residual."):].split(".")[0]) for k in sd if k.startswith(f"{p}residual.")}

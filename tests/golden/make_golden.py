@@ -10,7 +10,7 @@ truncation / loss logic is the reference's own).  Every weight comes from
 image_super_resolution_amd.weights.synth_state_dict, so tests rebuild the same
 weights from (key, shape, seed) instead of storing them.
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--only-denoise]
 """
 from __future__ import annotations
 
@@ -208,9 +208,31 @@ def main():
     ema = M.ModelEMA(nn.Linear(2, 2), tau=2000)
     ups = np.array([1, 10, 100, 1000, 5000])
     np.savez_compressed(OUT / "ema.npz", updates=ups, decay=np.array([ema.decay(int(u)) for u in ups]), tau=2000)
+    golden_denoise(M)
     print("done")
+
+
+def golden_denoise(M):
+    """10. Denoise (utils/models.py:672-706), eval, fp32: the network
+    `train.py --train_denoise` trains (train.py:204-205).  residual_blocks=4 →
+    2 + 2 + 2 ResidualBlock1; input 40x72 (even, not a tile multiple)."""
+    torch.manual_seed(0)
+    with torch.no_grad():
+        model = load_synth(M.Denoise(4).eval(), 30)
+        g = torch.Generator().manual_seed(31)
+        x = torch.rand(2, 3, 40, 72, generator=g) * 2 - 1
+        y = model(x.clone())
+    np.savez_compressed(OUT / "denoise.npz", x=np32(x), y=np32(y), seed=30, residual_blocks=4)
+    print("denoise", tuple(y.shape))
 
 
 if __name__ == "__main__":
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
-    main()
+    if sys.argv[1:2] == ["--only-denoise"]:  # regenerate just this fixture
+        if not REF.exists():
+            raise SystemExit("reference not present")
+        install_stubs()
+        import utils.models as _M  # reference
+        golden_denoise(_M)
+    else:
+        main()

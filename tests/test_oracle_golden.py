@@ -133,3 +133,16 @@ def test_ema_decay_matches_reference(golden):
     g = golden("ema")
     for u, d in zip(g["updates"], g["decay"]):
         assert abs(R.ema_decay(int(u), float(g["tau"])) - d) < 1e-12
+
+
+def test_denoise_matches_reference(golden):
+    """Denoise (utils/models.py:672-706): state_dict schema of the mirror class and
+    the oracle's forward against the reference run on the same synthetic weights."""
+    g = golden("denoise")
+    m = models.Denoise(int(g["residual_blocks"]))
+    sd = _sd(m, int(g["seed"]))
+    assert "residual_conv0.conv.bias" in sd and "conv2.0.conv.weight" in sd and "residual_1.1.m.1.bn.running_var" in sd
+    y = R.denoise(sd, t(g["x"]))
+    np.testing.assert_allclose(y.numpy(), g["y"], rtol=0, atol=2e-5)
+    # Model.fuse equivalence: folded BN gives the same output
+    np.testing.assert_allclose(R.denoise(R.fuse_state_dict(sd), t(g["x"])).numpy(), g["y"], rtol=0, atol=5e-5)
