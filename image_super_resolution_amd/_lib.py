@@ -108,6 +108,7 @@ SIGNATURES = {
     "isr_wgrad9x9": (c_int32, [POINTER(IsrWgrad9Desc), c_void_p, c_size_t, c_void_p]),
     "isr_ew_combine": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
     "isr_pixel_shuffle2": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
+    "isr_pixel_unshuffle2": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
     "isr_bn_stats": (c_int32, [POINTER(IsrBnDesc), c_void_p]),
     "isr_bn_finalize": (c_int32, [POINTER(IsrBnDesc), c_void_p]),
     "isr_bn_apply": (c_int32, [POINTER(IsrBnDesc), c_void_p]),

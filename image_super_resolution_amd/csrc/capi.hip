@@ -23,6 +23,7 @@ int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale
 int conv3x3_pack_batch(const isr_pack_item* items, int n, hipStream_t s);
 int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s);
 int pixel_shuffle2_dispatch(const isr_ew_desc* d, hipStream_t s);
+int pixel_unshuffle2_dispatch(const isr_ew_desc* d, hipStream_t s);
 int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s);
 int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s);
 int blocked_to_nchw_dispatch(const isr_convert_desc* d, hipStream_t s);
@@ -364,6 +365,20 @@ int isr_pixel_shuffle2(const isr_ew_desc* d, isr_stream_t s) {
         !view_ok(d->a, d->ha / 2, d->wa / 2, 0, 4 * d->c, "pixel_shuffle2.a", 1))
         return ISR_ERR_BAD_DESC;
     return launched(isr::pixel_shuffle2_dispatch(d, (hipStream_t)s), "pixel_shuffle2");
+}
+
+int isr_pixel_unshuffle2(const isr_ew_desc* d, isr_stream_t s) {
+    if (!d) return fail(ISR_ERR_BAD_DESC, "pixel_unshuffle2: null descriptor");
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0 || d->c % 64)
+        return fail(ISR_ERR_BAD_DESC, "pixel_unshuffle2: bad problem n=%d h=%d w=%d c=%d (c %% 64 == 0)", d->n, d->h,
+                    d->w, d->c);
+    if (d->ha < d->h || d->wa < d->w) return fail(ISR_ERR_BAD_DESC, "pixel_unshuffle2: computed region smaller than valid");
+    if (d->b.data) return fail(ISR_ERR_UNSUPPORTED, "pixel_unshuffle2: takes no b operand");
+    if (!view_ok(d->y, d->ha, d->wa, 0, d->c, "pixel_unshuffle2.y", 1) ||
+        !view_ok(d->a, 2 * d->ha, 2 * d->wa, 0, d->c / 4, "pixel_unshuffle2.a", 1))
+        return ISR_ERR_BAD_DESC;
+    if (d->m.data && !view_ok(d->m, 2 * d->ha, 2 * d->wa, 0, d->c / 4, "pixel_unshuffle2.m", 1)) return ISR_ERR_BAD_DESC;
+    return launched(isr::pixel_unshuffle2_dispatch(d, (hipStream_t)s), "pixel_unshuffle2");
 }
 
 static int convert_validate(const isr_convert_desc* d, const char* who) {

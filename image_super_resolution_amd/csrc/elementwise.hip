@@ -78,6 +78,57 @@ __global__ __launch_bounds__(256) void pixel_shuffle2_kernel(isr_ew_desc d) {
     }
 }
 
+// Its transpose (isr_pixel_unshuffle2): y[4c + s] at (y, x) = sa * a[c] at (2y + s/2, 2x + s%2),
+// times LeakyReLU'(m) there when m is given.  One thread per (output pixel, 8 source
+// channels): four 16-byte source loads (one per sub-pixel), four 16-byte stores of the
+// 32 output channels 4c0 .. 4c0 + 31.
+__global__ __launch_bounds__(256) void pixel_unshuffle2_kernel(isr_ew_desc d) {
+    const int cg = d.c / 32;
+    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        size_t r = i;
+        const int x = r % d.wa; r /= d.wa;
+        const int y = r % d.ha; r /= d.ha;
+        const int g = r % cg;
+        const int img = (int)(r / cg);
+        const int c0 = g * 8;  // first source channel
+        float t[4][8];
+        if (y < d.h && x < d.w) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int yy = 2 * y + (s >> 1), xx = 2 * x + (s & 1);
+                load8_bf16(view_at(d.a, img, yy, xx, c0), t[s]);
+                float mm[8];
+                if (d.m.data) load8_bf16(view_at(d.m, img, yy, xx, c0), mm);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    t[s][k] *= d.sa;
+                    if (d.m.data && !(mm[k] > 0.f)) t[s][k] *= d.mslope;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t[s][k] = 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // output channels 4c0 + 8q .. +7 = (c0 + 2q + j/4, s = j%4)
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = t[j & 3][2 * q + (j >> 2)];
+            store8_bf16(view_at(d.y, img, y, x, 4 * c0 + 8 * q), v);
+        }
+    }
+}
+
+int pixel_unshuffle2_dispatch(const isr_ew_desc* d, hipStream_t s) {
+    const size_t total = (size_t)d->n * d->ha * d->wa * (d->c / 32);
+    const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    hipLaunchKernelGGL(pixel_unshuffle2_kernel, dim3(blocks), dim3(256), 0, s, *d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int pixel_shuffle2_dispatch(const isr_ew_desc* d, hipStream_t s) {
     const size_t total = (size_t)d->n * d->ha * d->wa * (d->c / 8);
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);

@@ -1,4 +1,4 @@
-"""Denoise network (utils/models.py:672-706) on libisr — inference.
+"""Denoise network (utils/models.py:672-706) on libisr — inference and training.
 
 The denoiser `train.py --train_denoise` builds (train.py:204-205) and whose
 older variant ships as the reference's model.pt.  Same-resolution image in,
@@ -152,3 +152,246 @@ def run_denoise(dw: DenoiseWeights, x: torch.Tensor) -> torch.Tensor:
         dw.buffers["plan"] = None
         plan = dw.buffers["plan"] = DenoisePlan(dw, n, h, w, x.device)
     return plan.run(x, torch.empty(plan.out_shape, dtype=torch.float32, device=x.device))
+
+
+# ===================================================================== training
+class _TLayer:
+    """One conv of the Denoise network in training: parameter refs + packed copies."""
+
+    def __init__(self, conv_mod, kind: str):
+        self.mod = conv_mod                      # reference Conv / ConvWithoutBN
+        self.w = conv_mod.conv.weight
+        self.b = conv_mod.conv.bias
+        bn = getattr(conv_mod, "bn", None)
+        self.bn = bn if isinstance(bn, torch.nn.BatchNorm2d) else None
+        self.kind = kind                         # "3x3", "s2" (stride 2), "head", "tail"
+        self.cout, self.cin = self.w.shape[:2]
+        self.fwd = self.bwd = None
+        self.bn_state = None
+
+    def params(self) -> list[torch.Tensor]:
+        out = [self.w] + ([self.b] if self.b is not None else [])
+        return out + ([self.bn.weight, self.bn.bias] if self.bn is not None else [])
+
+    def pack(self) -> None:
+        w = self.w.detach().float()
+        if self.kind == "3x3":
+            self.fwd = ops.pack_conv3x3(w, out=self.fwd)
+            self.bwd = ops.pack_conv3x3_dgrad(w, out=self.bwd)
+        elif self.kind == "s2":
+            from .discriminator import expand_dgrad
+            self.fwd = ops.pack_conv3x3(expand_fwd(w), out=self.fwd)
+            self.bwd = ops.pack_conv3x3(expand_dgrad(w), out=self.bwd)
+        elif self.kind == "head":
+            self.fwd = ops.pack_head9x9(w, out=self.fwd)
+        else:  # tail: its input gradient is a head9x9 conv with 180°-rotated, transposed weights
+            self.fwd = ops.pack_tail9x9(w, out=self.fwd)
+            self.bwd = ops.pack_head9x9(w.flip(2, 3).transpose(0, 1).contiguous(), out=self.bwd)
+
+
+class _TBlock:
+    """ResidualBlock1 (utils/models.py:202-209) with its saved activations."""
+
+    def __init__(self, blk, n, h, w, c, dev, ha, wa, out_sub: dict):
+        self.a, self.b = _TLayer(blk.m[0], "3x3"), _TLayer(blk.m[1], "3x3")
+        self.Za = ActBuffer.alloc(n, h, w, c, 0, dev, ha=ha, wa=wa)
+        self.Ha = ActBuffer.alloc(n, h, w, c, 1, dev, ha=ha, wa=wa)
+        self.Zb = ActBuffer.alloc(n, h, w, c, 0, dev, ha=ha, wa=wa)
+        self.Y = ActBuffer.alloc(n, h, w, c, 2 if out_sub else 1, dev, ha=ha, wa=wa, **out_sub)
+        for l in (self.a, self.b):
+            if l.bn is None:
+                raise NotImplementedError("ResidualBlock1 training expects Conv layers with BatchNorm (unfused)")
+            l.bn_state = ops.BNState(c, dev)
+
+
+class DenoiseTrainPlan:
+    """Train-mode forward (BatchNorm on batch statistics, running stats updated) and
+    backward of Denoise on libisr for a fixed [n, 3, h, w] input.
+
+    Backward per ResidualBlock1 (reverse): BN_b backward on the block-output
+    gradient, wgrad(Ha), dgrad with LeakyReLU'(Ha) in the epilogue, BN_a backward,
+    wgrad(X), dgrad + the skip gradient (r1) → the block-input gradient.  The
+    stride-2 conv: wgrad over the x_sub2 view (taps {0,1}²) gathered to 3x3, dgrad
+    as the 2x2-tap conv with the PixelShuffle store (discriminator.py); the
+    PixelShuffle + LeakyReLU: isr_pixel_unshuffle2 with the LeakyReLU' mask;
+    the tail: tanh' then wgrad9x9 and a head9x9 dgrad; the head: wgrad9x9 on the
+    masked trunk gradient (ew_combine of chain + trunk)."""
+
+    def __init__(self, model, n: int, h: int, w: int, device):
+        if h % 2 or w % 2:
+            raise ValueError(f"Denoise needs an even input size, got {h}x{w}")
+        dev = self.device = torch.device(device)
+        self.key = (n, h, w, str(dev))
+        self.busy = False
+        h2, w2 = h // 2, w // 2
+        ha2, wa2 = round_up(h2, ops.TILE_H), round_up(w2, ops.TILE_W)
+        sub = dict(min_hp=2 * ha2 + 4, min_wp=2 * wa2 + 4)
+        self.head = _TLayer(model.conv0[0], "head")
+        self.down = _TLayer(model.residual_conv0, "s2")
+        self.conv1 = _TLayer(model.conv1, "3x3")
+        self.tail = _TLayer(model.conv2[0], "tail")
+        if self.conv1.bn is None:
+            raise NotImplementedError("Denoise training expects an unfused model (Conv layers with BatchNorm)")
+        self.conv1.bn_state = ops.BNState(64, dev)
+        self.F = ActBuffer.alloc(n, h, w, 64, 2, dev, **sub)
+        self.res0 = [_TBlock(b, n, h, w, 64, dev, None, None, sub) for b in model.residual_0]
+        self.Q0 = ActBuffer.alloc(n, h2, w2, 256, 1, dev, ha=ha2, wa=wa2)
+        self.res1 = [_TBlock(b, n, h2, w2, 256, dev, ha2, wa2, {}) for b in model.residual_1]
+        self.S = ActBuffer.alloc(n, h, w, 64, 1, dev, min_hp=2 * ha2 + 2, min_wp=2 * wa2 + 2)  # unshuffle mask
+        self.res2 = [_TBlock(b, n, h, w, 64, dev, None, None, {}) for b in model.residual_2]
+        self.Z1 = ActBuffer.alloc(n, h, w, 64, 0, dev)
+        self.T = ActBuffer.alloc(n, h, w, 64, 4, dev)
+        # gradient scratch: full resolution (slack for the stride-2 dgrad's shuffled store) and half
+        self.gf = [ActBuffer.alloc(n, h, w, 64, 1, dev, min_hp=2 * ha2 + 2, min_wp=2 * wa2 + 2) for _ in range(5)]
+        self.gq = [ActBuffer.alloc(n, h2, w2, 256, 1, dev, ha=ha2, wa=wa2) for _ in range(4)]
+        self.out_shape = (n, 3, h, w)
+        self.layers = ([self.head] + [l for b in self.res0 for l in (b.a, b.b)] + [self.down]
+                       + [l for b in self.res1 for l in (b.a, b.b)] + [l for b in self.res2 for l in (b.a, b.b)]
+                       + [self.conv1, self.tail])
+        self.x = self.y = None
+
+    def params(self) -> list[torch.Tensor]:
+        return [p for l in self.layers for p in l.params()]
+
+    def pack(self) -> None:
+        for l in self.layers:
+            l.pack()
+
+    # ----------------------------------------------------------------- forward
+    @staticmethod
+    def _bn_fwd(l: _TLayer, z: ActBuffer, y: ActBuffer, c: int, **kw) -> None:
+        ops.bn_forward(ops.bn_desc(z, y, c, l.bn_state, l.bn, **kw), l.bn_state)
+        if l.bn.num_batches_tracked is not None:
+            l.bn.num_batches_tracked.add_(1)
+
+    def _chain_fwd(self, blocks, x: ActBuffer, c: int) -> ActBuffer:
+        for b in blocks:
+            ops.conv3x3(x, c, b.a.fwd, None, c, b.Za, slope=1.0)
+            self._bn_fwd(b.a, b.Za, b.Ha, c, slope=SLOPE)
+            ops.conv3x3(b.Ha, c, b.b.fwd, None, c, b.Zb, slope=1.0)
+            self._bn_fwd(b.b, b.Zb, b.Y, c, slope=1.0, r1=x, s1=1.0)
+            x = b.Y
+        return x
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        self.x = x = x.float().contiguous()
+        ops.head9x9(x, self.head.fwd, self.head.b.detach(), self.F, slope=SLOPE)
+        self.x_last0 = self._chain_fwd(self.res0, self.F, 64)
+        ops.conv3x3(self.x_last0, 256, self.down.fwd, self.down.b.detach(), 256, self.Q0, slope=SLOPE,
+                    x_sub2=True, taps=1)
+        self.q_last = self._chain_fwd(self.res1, self.Q0, 256)
+        ops.pixel_shuffle2(self.S, self.q_last, 64, slope=SLOPE)
+        self.r_last = self._chain_fwd(self.res2, self.S, 64)
+        ops.conv3x3(self.r_last, 64, self.conv1.fwd, None, 64, self.Z1, slope=1.0)
+        self._bn_fwd(self.conv1, self.Z1, self.T, 64, slope=1.0, r1=self.F, s1=1.0)
+        y = torch.empty(self.out_shape, device=self.device)
+        ops.tail9x9(self.T, self.tail.fwd, self.tail.b.detach(), y)
+        self.y = y
+        return y
+
+    # ----------------------------------------------------------------- backward
+    def _bn_bwd(self, l: _TLayer, z: ActBuffer, g: ActBuffer, dz: ActBuffer, c: int, grads: dict) -> None:
+        dgam = torch.empty(c, device=self.device)
+        dbet = torch.empty(c, device=self.device)
+        ops.bn_backward(ops.bn_desc(z, g, c, l.bn_state, l.bn, dz=dz, dgamma=dgam, dbeta=dbet,
+                                    update_running=False), l.bn_state)
+        grads[id(l.bn.weight)], grads[id(l.bn.bias)] = dgam, dbet
+
+    def _wgrad(self, l: _TLayer, x: ActBuffer, g: ActBuffer, grads: dict) -> None:
+        dw = torch.empty(l.cout, l.cin, 3, 3, device=self.device)
+        ops.wgrad3x3(x, l.cin, g, l.cout, dw, None)
+        grads[id(l.w)] = dw
+
+    def _chain_bwd(self, blocks, x_in: ActBuffer, g: ActBuffer, pool: list, c: int, grads: dict,
+                   m_in: ActBuffer | None = None) -> ActBuffer:
+        """Reverse through a ResidualBlock1 chain; g = gradient wrt the chain output.
+        Returns the gradient wrt the chain input (times LeakyReLU'(m_in) when given).
+        `pool` holds four scratch buffers of the chain's grid (g may be one of them)."""
+        for i in range(len(blocks) - 1, -1, -1):
+            b = blocks[i]
+            xi = blocks[i - 1].Y if i > 0 else x_in
+            dz, gh, gin = [p for p in pool if p is not g][:3]
+            self._bn_bwd(b.b, b.Zb, g, dz, c, grads)
+            self._wgrad(b.b, b.Ha, dz, grads)
+            ops.conv3x3(dz, c, b.b.bwd, None, c, gh, slope=1.0, m=b.Ha, mslope=SLOPE)
+            self._bn_bwd(b.a, b.Za, gh, dz, c, grads)
+            self._wgrad(b.a, xi, dz, grads)
+            mk = dict(m=m_in, mslope=SLOPE) if (i == 0 and m_in is not None) else {}
+            ops.conv3x3(dz, c, b.a.bwd, None, c, gin, slope=1.0, r1=g, s1=1.0, **mk)
+            g = gin
+        if not blocks and m_in is not None:
+            raise NotImplementedError("masked chain input needs at least one block")
+        return g
+
+    def backward(self, gy: torch.Tensor) -> dict:
+        from .discriminator import gather_wgrad
+        dev = self.device
+        grads: dict = {}
+        gp = (gy.float() * (1.0 - self.y * self.y)).contiguous()  # tanh' (utils/models.py:692, act=nn.Tanh())
+        # tail (conv2): weight / bias gradient, input gradient by the head kernel
+        dw2 = torch.empty(3, 64, 9, 9, device=dev)
+        db2 = torch.empty(3, device=dev)
+        ops.wgrad9x9(gp, self.T, dw2, db2, head=False)
+        grads[id(self.tail.w)], grads[id(self.tail.b)] = dw2, db2
+        gT, pool = self.gf[4], self.gf[:4]
+        ops.head9x9(gp, self.tail.bwd, None, gT, slope=1.0)
+        # conv1 (+BN) — gT also reaches F through the trunk residual
+        f0, f1 = pool[0], pool[1]
+        self._bn_bwd(self.conv1, self.Z1, gT, f0, 64, grads)
+        self._wgrad(self.conv1, self.r_last, f0, grads)
+        ops.conv3x3(f0, 64, self.conv1.bwd, None, 64, f1, slope=1.0)
+        # residual_2, then PixelShuffle(2) + LeakyReLU backward into the half grid
+        g = self._chain_bwd(self.res2, self.S, f1, pool, 64, grads)
+        gq = self.gq[0]
+        ops.pixel_unshuffle2(gq, g, 256, m=self.S, mslope=SLOPE)
+        # residual_1; its first block's input gradient is masked by LeakyReLU'(Q0)
+        g = self._chain_bwd(self.res1, self.Q0, gq, self.gq, 256, grads, m_in=self.Q0)
+        # stride-2 conv: weight (+bias) gradient on the phase view, input gradient by the shuffled store
+        dwp = torch.empty(256, 256, 3, 3, device=dev)
+        db = torch.empty(256, device=dev)
+        ops.wgrad3x3(self.x_last0, 256, g, 256, dwp, db, x_sub2=True, taps=1)
+        grads[id(self.down.w)], grads[id(self.down.b)] = gather_wgrad(dwp, 64), db
+        gx = pool[0]
+        ops.conv3x3(g, 256, self.down.bwd, None, 256, gx, slope=1.0, shuffle=2, taps=2)
+        # residual_0, then the trunk: g_F = chain + gT, times LeakyReLU'(F) (conv0's act)
+        g = self._chain_bwd(self.res0, self.F, gx, pool, 64, grads)
+        gF = next(p for p in pool if p is not g)
+        ops.ew_combine(gF, g, 64, sa=1.0, b=gT, sb=1.0, m=self.F, mslope=SLOPE)
+        dw0 = torch.empty(64, 3, 9, 9, device=dev)
+        db0 = torch.empty(64, device=dev)
+        ops.wgrad9x9(self.x, gF, dw0, db0, head=True)
+        grads[id(self.head.w)], grads[id(self.head.b)] = dw0, db0
+        return grads
+
+
+class _DenoiseFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan, *params):
+        y = plan.forward(x)
+        ctx.plan = plan
+        plan.busy = True
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        plan = ctx.plan
+        grads = plan.backward(gy.contiguous())
+        plan.busy = False
+        return (None, None, *[grads.get(id(p)) for p in plan.params()])
+
+
+def train_forward(model, x: torch.Tensor) -> torch.Tensor:
+    """Differentiable train-mode Denoise forward on libisr (train.py:52-63 with
+    --train_denoise).  One plan per input geometry; the graph of one call must be
+    backpropagated before the next call (the plan holds its activations)."""
+    n, _, h, w = x.shape
+    key = (n, h, w, str(x.device))
+    plan = model.__dict__.get("_isr_train_plan")
+    if plan is None or plan.key != key:
+        model.__dict__["_isr_train_plan"] = None
+        plan = model.__dict__["_isr_train_plan"] = DenoiseTrainPlan(model, n, h, w, x.device)
+    if plan.busy:
+        raise RuntimeError("Denoise train_forward: the previous forward's graph was not backpropagated")
+    plan.pack()
+    with torch.autocast("cuda", enabled=False):
+        return _DenoiseFn.apply(x.float(), plan, *plan.params())

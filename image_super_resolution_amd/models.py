@@ -333,7 +333,10 @@ class Denoise(nn.Module):
 
     def forward(self, inputs: torch.Tensor) -> torch.Tensor:
         _require_cuda(inputs, "Denoise")
-        _no_train(self, "Denoise")
+        if self.training and torch.is_grad_enabled():
+            # differentiable HIP path: train-mode BatchNorm, libisr backward (train.py:52-63)
+            from .denoise import train_forward
+            return train_forward(self, inputs)
         from .denoise import run_denoise
         return run_denoise(self._packed(inputs.device), inputs)
 

@@ -343,6 +343,7 @@ def launch_wgrad3x3(d: IsrWgradDesc, device) -> None:
     nbytes = lib.isr_wgrad3x3_workspace_bytes(ctypes.byref(d))
     if nbytes == 0:
         check(lib.isr_wgrad3x3(ctypes.byref(d), None, 0, _stream()), "isr_wgrad3x3")
+        return
     ws = _WS.get(nbytes, device)
     check(lib.isr_wgrad3x3(ctypes.byref(d), ws.data_ptr(), ws.numel(), _stream()), "isr_wgrad3x3")
 
@@ -382,6 +383,7 @@ def launch_wgrad9x9(d: IsrWgrad9Desc, device) -> None:
     nbytes = lib.isr_wgrad9x9_workspace_bytes(ctypes.byref(d))
     if nbytes == 0:
         check(lib.isr_wgrad9x9(ctypes.byref(d), None, 0, _stream()), "isr_wgrad9x9")
+        return
     ws = _WS.get(nbytes, device)
     check(lib.isr_wgrad9x9(ctypes.byref(d), ws.data_ptr(), ws.numel(), _stream()), "isr_wgrad9x9")
 
@@ -414,6 +416,22 @@ def pixel_shuffle2_desc(y: ActBuffer, a: ActBuffer, c: int, *, slope: float = 1.
     d.y, d.a, d.b, d.m = y.view(0), a.view(0), _NULL_VIEW, _NULL_VIEW
     d.sa, d.sb, d.mslope = sa, 0.0, slope
     return d
+
+
+def pixel_unshuffle2_desc(y: ActBuffer, a: ActBuffer, c: int, *, m: ActBuffer | None = None, mslope: float = 1.0,
+                          sa: float = 1.0) -> IsrEwDesc:
+    """y[0:c] (grid h x w) = PixelShuffle(2)ᵀ(sa * a[0:c/4] * LeakyReLU'(m)) — a, m on the 2h x 2w grid."""
+    d = IsrEwDesc()
+    d.n, d.h, d.w, d.ha, d.wa, d.c = y.n, y.h, y.w, y.ha, y.wa, c
+    d.y, d.a, d.b = y.view(0), a.view(0), _NULL_VIEW
+    d.m = m.view(0) if m is not None else _NULL_VIEW
+    d.sa, d.sb, d.mslope = sa, 0.0, mslope
+    return d
+
+
+def pixel_unshuffle2(y: ActBuffer, a: ActBuffer, c: int, **kw) -> None:
+    check(_lib.load().isr_pixel_unshuffle2(ctypes.byref(pixel_unshuffle2_desc(y, a, c, **kw)), _stream()),
+          "isr_pixel_unshuffle2")
 
 
 def pixel_shuffle2(y: ActBuffer, a: ActBuffer, c: int, **kw) -> None:

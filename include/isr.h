@@ -203,6 +203,12 @@ int isr_ew_combine(const isr_ew_desc* d, isr_stream_t s);
  * (utils/models.py:687) applied to the output of a ResidualBlock1 (:202-209),
  * whose residual add precedes the shuffle so it cannot ride a conv epilogue. */
 int isr_pixel_shuffle2(const isr_ew_desc* d, isr_stream_t s);
+/* Its transpose, the PixelShuffle(2) input gradient (Denoise training, train.py:204-205):
+ *   y[4c + s] at (y, x) = sa * a[c] at (2y + s/2, 2x + s%2) * (m there > 0 ? 1 : mslope)
+ * (n, h, w, ha, wa) is the OUTPUT (half-resolution) grid, d->c its channel count
+ * (multiple of 64); a and the optional LeakyReLU' mask source m hold c/4 channels on
+ * the 2h x 2w grid (rows / cols up to 2ha / 2wa are read); b must be NULL. */
+int isr_pixel_unshuffle2(const isr_ew_desc* d, isr_stream_t s);
 
 /* Layout conversion between NCHW fp32 tensors and channel-blocked views
  * (network / loss boundaries: the VGG19 input, utils/loss.py:16-24, and the

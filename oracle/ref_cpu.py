@@ -87,13 +87,13 @@ def generator(sd: dict, x: torch.Tensor, *, num_blocks: int, scale: int, enchant
     return torch.tanh(F.conv2d(y, w, sd[f"{p}conv2.conv.bias"], padding=w.shape[-1] // 2))
 
 
-def residual_block1(sd: dict, prefix: str, x: torch.Tensor, slope: float = 0.2) -> torch.Tensor:
+def residual_block1(sd: dict, prefix: str, x: torch.Tensor, slope: float = 0.2, train_bn: bool = False) -> torch.Tensor:
     """ResidualBlock1.forward (utils/models.py:202-209): x + Conv(act=False)(Conv(act)(x))."""
-    h = conv_unit(sd, f"{prefix}.m.0", x, slope)
-    return x + conv_unit(sd, f"{prefix}.m.1", h, None)
+    h = conv_unit(sd, f"{prefix}.m.0", x, slope, train_bn)
+    return x + conv_unit(sd, f"{prefix}.m.1", h, None, train_bn)
 
 
-def denoise(sd: dict, x: torch.Tensor) -> torch.Tensor:
+def denoise(sd: dict, x: torch.Tensor, train_bn: bool = False) -> torch.Tensor:
     """Denoise.forward (utils/models.py:695-706); every act is LeakyReLU(0.2) (:676-690).
 
     conv0 9x9 → residual_0 → residual_conv0 (3x3 stride 2, pad 1, +bias, act)
@@ -101,7 +101,7 @@ def denoise(sd: dict, x: torch.Tensor) -> torch.Tensor:
     def chain(name, y):
         n = len({int(k[len(name) + 1:].split(".")[0]) for k in sd if k.startswith(name + ".")})
         for i in range(n):
-            y = residual_block1(sd, f"{name}.{i}", y)
+            y = residual_block1(sd, f"{name}.{i}", y, train_bn=train_bn)
         return y
 
     feat = conv_unit(sd, "conv0.0", x, 0.2)
@@ -111,7 +111,7 @@ def denoise(sd: dict, x: torch.Tensor) -> torch.Tensor:
     r = chain("residual_1", r)
     r = F.leaky_relu(F.pixel_shuffle(r, 2), 0.2)
     r = chain("residual_2", r)
-    y = feat + conv_unit(sd, "conv1", r, None)
+    y = feat + conv_unit(sd, "conv1", r, None, train_bn)
     w = sd["conv2.0.conv.weight"]
     return torch.tanh(F.conv2d(y, w, sd["conv2.0.conv.bias"], padding=w.shape[-1] // 2))
 
