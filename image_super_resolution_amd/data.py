@@ -88,6 +88,34 @@ class GPUTransform:
         return hr.contiguous(), lr.contiguous()
 
 
+class NoisyTransform:
+    """Batched (clean, noisy) pairs for `train.py --train_denoise` from uint8 crops
+    on the device (Noisy_dataset, utils/datasets.py:361-389): clean = 2*crop/255 - 1;
+    noisy = Normalize(GaussNoise(crop)), albumentations GaussNoise defaults
+    (var_limit (10, 50) on the 0-255 scale, per-channel, p = 0.5 per sample, result
+    clipped to [0, 255]).  The reference's ISONoise and ImageCompression (also p = 0.5)
+    need a host JPEG codec / HLS conversion and are not reproduced."""
+
+    def __init__(self, mean=IMAGENET_MEAN, std=IMAGENET_STD, var_limit=(10.0, 50.0), p: float = 0.5,
+                 device="cuda", seed: int = 0):
+        self.mean = torch.tensor(mean, device=device).view(1, 3, 1, 1)
+        self.std = torch.tensor(std, device=device).view(1, 3, 1, 1)
+        self.var_limit, self.p, self.device = var_limit, p, device
+        self.gen = torch.Generator(device=device).manual_seed(seed)
+
+    def __call__(self, crops_u8: torch.Tensor):
+        x = crops_u8.to(self.device, non_blocking=True).float()
+        n = x.shape[0]
+        g = self.gen
+        var = torch.empty(n, 1, 1, 1, device=self.device).uniform_(*self.var_limit, generator=g)
+        apply = (torch.rand(n, 1, 1, 1, device=self.device, generator=g) < self.p).float()
+        noise = torch.randn(x.shape, device=self.device, generator=g) * var.sqrt() * apply
+        noisy = (x + noise).clamp_(0, 255).div_(255.0)
+        lr = (noisy - self.mean) / self.std
+        hr = x / 255.0 * 2.0 - 1.0
+        return hr.contiguous(), lr.contiguous()
+
+
 class SyntheticSR:
     """Endless synthetic uint8 HR crops on the GPU: bicubic-upsampled 32x32
     uniform noise (a smooth 'natural-ish' image), seed per batch and rank."""

@@ -223,6 +223,7 @@ class DenoiseTrainPlan:
         dev = self.device = torch.device(device)
         self.key = (n, h, w, str(dev))
         self.busy = False
+        self.grad_group = None
         h2, w2 = h // 2, w // 2
         ha2, wa2 = round_up(h2, ops.TILE_H), round_up(w2, ops.TILE_W)
         sub = dict(min_hp=2 * ha2 + 4, min_wp=2 * wa2 + 4)
@@ -377,7 +378,18 @@ class _DenoiseFn(torch.autograd.Function):
         plan = ctx.plan
         grads = plan.backward(gy.contiguous())
         plan.busy = False
-        return (None, None, *[grads.get(id(p)) for p in plan.params()])
+        out = [grads.get(id(p)) for p in plan.params()]
+        if plan.grad_group is not None:  # data parallel: one flat RCCL all-reduce (mean), as DDP
+            import torch.distributed as dist
+            grp = None if plan.grad_group is True else plan.grad_group
+            flat = torch.cat([g.reshape(-1) for g in out])
+            dist.all_reduce(flat, group=grp)
+            flat.div_(dist.get_world_size(grp))
+            off = 0
+            for i, g in enumerate(out):
+                out[i] = flat[off:off + g.numel()].view_as(g)
+                off += g.numel()
+        return (None, None, *out)
 
 
 def train_forward(model, x: torch.Tensor) -> torch.Tensor:
@@ -393,5 +405,6 @@ def train_forward(model, x: torch.Tensor) -> torch.Tensor:
     if plan.busy:
         raise RuntimeError("Denoise train_forward: the previous forward's graph was not backpropagated")
     plan.pack()
+    plan.grad_group = model.__dict__.get("_isr_grad_group")  # train_engine.enable_grad_allreduce
     with torch.autocast("cuda", enabled=False):
         return _DenoiseFn.apply(x.float(), plan, *plan.params())

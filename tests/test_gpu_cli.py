@@ -58,3 +58,28 @@ def test_train_then_upscale(tmp_path):
     still = np.asarray(Image.open(tmp_path / "f0_out.png"))
     assert np.array_equal(vid[0][..., ::-1], still)
     torch.cuda.synchronize()
+
+
+def test_train_denoise_cli(tmp_path):
+    """`train.py --train_denoise` (train.py:204-243): Denoise on libisr, MSE on
+    synthetic noisy/clean pairs, checkpoint denoise_{save_name}_{rs_deep}_{add_rate}.pt,
+    and a second run picks it up (the reference restarts at epoch 0 when the
+    checkpoint holds no optimiser state, train.py:214-219)."""
+    import train
+    from image_super_resolution_amd import checkpoint, models
+
+    common = ["--train_denoise", "--synthetic", "--steps", "6", "--batch_size", "2", "--shape", "48", "--rs_deep",
+              "2", "--lr", "1e-3", "--work_dir", str(tmp_path), "--save_name", "d"]
+    train.main(train.parse(common + ["--epochs", "1"]))
+    ck_path = tmp_path / "denoise_d_2_0.2.pt"
+    ck = checkpoint.load_checkpoint(ck_path)
+    assert ck["epoch"] == 0 and ck["optimizer"] is None  # last epoch of the run: no optimiser state (reference)
+    m = models.Denoise(2)
+    m.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ck["gen_net"].items()})
+    assert int(m.conv1.bn.num_batches_tracked) == 6
+    train.main(train.parse(common + ["--epochs", "2"]))
+    ck2 = checkpoint.load_checkpoint(ck_path)
+    assert ck2["epoch"] == 1
+    # the trained denoiser runs through the inference plan
+    y = m.eval().cuda()(torch.rand(1, 3, 32, 32, device="cuda") * 2 - 1)
+    assert y.shape == (1, 3, 32, 32) and torch.isfinite(y).all()

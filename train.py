@@ -97,8 +97,40 @@ def main(opt):
     scaler_gen = torch.amp.GradScaler("cuda", enabled=False)  # bf16: no loss scaling needed
     scaler_dis = torch.amp.GradScaler("cuda", enabled=False)
 
-    if opt.train_denoise:
-        raise NotImplementedError("--train_denoise: the Denoise network is outside the HIP hot path (SURVEY §8f)")
+    if opt.train_denoise:  # train.py:204-243 of the reference
+        dn_ck = work_dir / f"denoise_{opt.save_name}_{opt.rs_deep}_{opt.add_rate}.pt"
+        model = models.Denoise(opt.rs_deep)
+        ema = models.ModelEMA(model, tau=opt.epochs * iters)
+        model.to(device)
+        ema.ema.to(device)
+        optimizer = optim.FusedAdam(model.parameters(), lr=opt.lr)
+        start = 0
+        if dn_ck.is_file():
+            ck = checkpoint.load_checkpoint(dn_ck)
+            print(f"load from {dn_ck.as_posix()}")
+            sd = checkpoint.intersect_dicts({k: v.float() if v.is_floating_point() else v
+                                             for k, v in ck["gen_net"].items()}, model.state_dict())
+            model.load_state_dict(sd, strict=False)
+            if len(sd) == len(model.state_dict()) and ck.get("optimizer") is not None:
+                optimizer.load_state_dict(ck["optimizer"])
+                start = ck["epoch"] + 1
+            print(f"Loaded pre-trained {len(sd)}/{len(model.state_dict())} model")
+        if group is not None:
+            enable_grad_allreduce(model, group)
+            for p in model.parameters():
+                torch.distributed.broadcast(p.data, 0)
+        schedule = torch.optim.lr_scheduler.LinearLR(optimizer, 1, opt.lr2, total_iters=opt.epochs * iters)
+        n_p = sum(p.numel() for p in model.parameters())
+        print(f"Model: {n_p:,} parameters, {n_p:,} gradients")
+        transform = data.NoisyTransform(mean, std, device=device, seed=opt.seed * 7 + rank)
+        for epoch in range(start, opt.epochs):
+            losses = trainer.train(model, ema, batches, transform, nn.MSELoss(), optimizer, scaler_gen, schedule,
+                                   epoch, writer, steps=iters)
+            if rank == 0:
+                print(f"epoch {epoch}: loss {np.mean(losses):.5f}")
+                checkpoint.save_checkpoint(dn_ck, gen_net=model, optimizer=optimizer.state_dict()
+                                           if epoch != opt.epochs - 1 else None, epoch=epoch, mean=mean, std=std)
+        return
 
     if opt.resnet:
         model = (models.EResNet(opt.rs_deep, opt.add_rate, opt.scale) if opt.enchant
