@@ -60,6 +60,13 @@ def _no_train(module: nn.Module, who: str):
                                   "train-mode autograd; module forward is the inference path")
 
 
+def _isr_free_state(module: nn.Module) -> dict:
+    """Module state without the libisr caches (`_isr_*`: packed weights, launch plans
+    holding ctypes descriptors), so deepcopy / pickling (ModelEMA, checkpoints) works
+    after a forward; the copy re-packs on its first call."""
+    return {k: v for k, v in module.__dict__.items() if not k.startswith("_isr_")}
+
+
 class Conv(nn.Module):
     """Conv2d(bias=False) + BatchNorm2d + act (utils/models.py:75-111)."""
     store_bn = nn.Identity()
@@ -196,6 +203,9 @@ class Scaler(nn.Module):
 class _Generator(nn.Module):
     enchant = False
 
+    def __getstate__(self):
+        return _isr_free_state(self)
+
     def _packed(self, device) -> engine.GeneratorWeights:
         key = (str(device),) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
         cache = self.__dict__.get("_isr_pack")
@@ -320,6 +330,9 @@ class Denoise(nn.Module):
         for x in self.modules():
             if hasattr(x, "inplace"):
                 x.inplace = True
+
+    def __getstate__(self):
+        return _isr_free_state(self)
 
     def _packed(self, device):
         from .denoise import pack_denoise

@@ -163,3 +163,19 @@ def test_pixel_unshuffle2_kernel_exact():
     ref = F.pixel_unshuffle(torch.where(mm > 0, a, a * 0.2), 2).to(torch.bfloat16).float()
     assert torch.equal(yb.to_nchw().cpu(), ref)
     assert int((yb.outside_valid() != 0).sum()) == 0
+
+
+def test_deepcopy_after_forward():
+    """ModelEMA deep-copies the model; libisr caches (ctypes descriptors) must not travel."""
+    from copy import deepcopy
+    m = _model(lambda: models.Denoise(2), 80).to(DEV)
+    x = torch.rand(1, 3, 32, 32, device=DEV) * 2 - 1
+    with torch.no_grad():
+        y = m(x)
+        c = deepcopy(m)
+        assert "_isr_pack" in m.__dict__ and "_isr_pack" not in c.__dict__
+        assert torch.equal(c(x), y)
+    g = _model(lambda: models.ResNet(1, 0.2, scaleRate=2), 81).to(DEV)
+    with torch.no_grad():
+        yg = g(x)
+        assert torch.equal(deepcopy(g)(x), yg)
