@@ -3,15 +3,24 @@
 // region (ha x wa), zeros written outside the valid h x w region.
 #include "isr_common.h"
 
+// Index type of the grid-stride elementwise kernels: 32-bit (cheap div/mod for the
+// pixel decomposition) whenever the element-group count leaves headroom for the stride.
+#define ISR_IDX_LAUNCH(K, total, grid, s, arg)                                          \
+    do {                                                                                \
+        if ((size_t)(total) < (1ull << 31)) hipLaunchKernelGGL(K<uint32_t>, grid, dim3(256), 0, s, arg); \
+        else hipLaunchKernelGGL(K<size_t>, grid, dim3(256), 0, s, arg);                \
+    } while (0)
+
 namespace isr {
 
+template <typename I>
 __global__ __launch_bounds__(256) void ew_combine_kernel(isr_ew_desc d) {
     const int cg = d.c / 8;
-    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const I total = (I)((size_t)d.n * d.ha * d.wa * cg);
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
         // channel group innermost within a 16-channel plane pair, then x, y, plane, image:
         // consecutive threads touch consecutive 16-byte units of one plane row.
-        size_t r = i;
+        I r = i;
         const int half = r % 2; r /= 2;
         const int x = r % d.wa; r /= d.wa;
         const int y = r % d.ha; r /= d.ha;
@@ -42,7 +51,7 @@ __global__ __launch_bounds__(256) void ew_combine_kernel(isr_ew_desc d) {
 int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s) {
     const size_t total = (size_t)d->n * d->ha * d->wa * (d->c / 8);
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-    hipLaunchKernelGGL(ew_combine_kernel, dim3(blocks), dim3(256), 0, s, *d);
+    ISR_IDX_LAUNCH(ew_combine_kernel, total, dim3(blocks), s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -51,11 +60,12 @@ int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s) {
 // (output pixel, 8 output channels): the 8 source channels 4c+s .. 4c+28+s are
 // gathered from the 32 channels (two 16-channel planes) at the source pixel; the
 // four sub-pixel threads of a source pixel re-read the same 64 bytes from L2.
+template <typename I>
 __global__ __launch_bounds__(256) void pixel_shuffle2_kernel(isr_ew_desc d) {
     const int cg = d.c / 8;
-    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        size_t r = i;
+    const I total = (I)((size_t)d.n * d.ha * d.wa * cg);
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+        I r = i;
         const int half = r % 2; r /= 2;
         const int x = r % d.wa; r /= d.wa;
         const int y = r % d.ha; r /= d.ha;
@@ -82,11 +92,12 @@ __global__ __launch_bounds__(256) void pixel_shuffle2_kernel(isr_ew_desc d) {
 // times LeakyReLU'(m) there when m is given.  One thread per (output pixel, 8 source
 // channels): four 16-byte source loads (one per sub-pixel), four 16-byte stores of the
 // 32 output channels 4c0 .. 4c0 + 31.
+template <typename I>
 __global__ __launch_bounds__(256) void pixel_unshuffle2_kernel(isr_ew_desc d) {
     const int cg = d.c / 32;
-    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        size_t r = i;
+    const I total = (I)((size_t)d.n * d.ha * d.wa * cg);
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+        I r = i;
         const int x = r % d.wa; r /= d.wa;
         const int y = r % d.ha; r /= d.ha;
         const int g = r % cg;
@@ -125,14 +136,14 @@ __global__ __launch_bounds__(256) void pixel_unshuffle2_kernel(isr_ew_desc d) {
 int pixel_unshuffle2_dispatch(const isr_ew_desc* d, hipStream_t s) {
     const size_t total = (size_t)d->n * d->ha * d->wa * (d->c / 32);
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-    hipLaunchKernelGGL(pixel_unshuffle2_kernel, dim3(blocks), dim3(256), 0, s, *d);
+    ISR_IDX_LAUNCH(pixel_unshuffle2_kernel, total, dim3(blocks), s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int pixel_shuffle2_dispatch(const isr_ew_desc* d, hipStream_t s) {
     const size_t total = (size_t)d->n * d->ha * d->wa * (d->c / 8);
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-    hipLaunchKernelGGL(pixel_shuffle2_kernel, dim3(blocks), dim3(256), 0, s, *d);
+    ISR_IDX_LAUNCH(pixel_shuffle2_kernel, total, dim3(blocks), s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -142,13 +153,14 @@ namespace isr {
 
 // NCHW fp32 → channel-blocked bf16 (channels [0, round16(c)), zero padded), with
 // optional per-channel affine and LeakyReLU' mask; zeros outside the valid region.
+template <typename I>
 __global__ __launch_bounds__(256) void nchw_to_blocked_kernel(isr_convert_desc d) {
     const int cp = (d.c + 15) / 16;
-    const size_t total = (size_t)d.n * cp * d.ha * d.wa;
+    const I total = (I)((size_t)d.n * cp * d.ha * d.wa);
     const size_t plane = (size_t)d.h * d.w;
     const float* src = (const float*)d.nchw;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        size_t r = i;
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+        I r = i;
         const int x = r % d.wa; r /= d.wa;
         const int y = r % d.ha; r /= d.ha;
         const int pl = r % cp;
@@ -185,11 +197,12 @@ __global__ __launch_bounds__(256) void nchw_to_blocked_kernel(isr_convert_desc d
 }
 
 // channel-blocked bf16 → NCHW fp32 (channels [0, c), valid region only)
+template <typename I>
 __global__ __launch_bounds__(256) void blocked_to_nchw_kernel(isr_convert_desc d) {
-    const size_t total = (size_t)d.n * d.c * d.h * d.w;
+    const I total = (I)((size_t)d.n * d.c * d.h * d.w);
     const size_t plane = (size_t)d.h * d.w;
     float* dst = (float*)d.nchw;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
         const int x = (int)(i % d.w);
         const int y = (int)((i / d.w) % d.h);
         const size_t ic = i / plane;
@@ -204,12 +217,13 @@ __global__ __launch_bounds__(256) void blocked_to_nchw_kernel(isr_convert_desc d
 
 // 2x2 / stride-2 max pool on blocked views (utils/models.py:454-510 via torchvision
 // vgg19.features MaxPool2d(2, 2)); output grid (h/2, w/2), computed region (ha_o, wa_o).
+template <typename I>
 __global__ __launch_bounds__(256) void maxpool2_fwd_kernel(isr_pool_desc d) {
     const int cg = d.c / 8;
     const int ho = d.h / 2, wo = d.w / 2;
-    const size_t total = (size_t)d.n * d.hao * d.wao * cg;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        size_t r = i;
+    const I total = (I)((size_t)d.n * d.hao * d.wao * cg);
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+        I r = i;
         const int half = r % 2; r /= 2;
         const int x = r % d.wao; r /= d.wao;
         const int y = r % d.hao; r /= d.hao;
@@ -233,12 +247,13 @@ __global__ __launch_bounds__(256) void maxpool2_fwd_kernel(isr_pool_desc d) {
 
 // backward: g_in at the first maximum of each window (PyTorch's scan order, row-major)
 // = g_out, times (x > 0 ? 1 : mslope) — the ReLU' of the layer that produced x.
+template <typename I>
 __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(isr_pool_desc d) {
     const int cg = d.c / 8;
     const int ho = d.h / 2, wo = d.w / 2;
-    const size_t total = (size_t)d.n * d.hao * d.wao * cg;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        size_t r = i;
+    const I total = (I)((size_t)d.n * d.hao * d.wao * cg);
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+        I r = i;
         const int half = r % 2; r /= 2;
         const int x = r % d.wao; r /= d.wao;
         const int y = r % d.hao; r /= d.hao;
@@ -274,20 +289,21 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(isr_pool_desc d) {
 static int blocks_for(size_t total) { return (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192); }
 
 int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s) {
-    hipLaunchKernelGGL(nchw_to_blocked_kernel, dim3(blocks_for((size_t)d->n * ((d->c + 15) / 16) * d->ha * d->wa)),
-                       dim3(256), 0, s, *d);
+    const size_t total = (size_t)d->n * ((d->c + 15) / 16) * d->ha * d->wa;
+    ISR_IDX_LAUNCH(nchw_to_blocked_kernel, total, dim3(blocks_for(total)), s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int blocked_to_nchw_dispatch(const isr_convert_desc* d, hipStream_t s) {
-    hipLaunchKernelGGL(blocked_to_nchw_kernel, dim3(blocks_for((size_t)d->n * d->c * d->h * d->w)), dim3(256), 0, s, *d);
+    const size_t total = (size_t)d->n * d->c * d->h * d->w;
+    ISR_IDX_LAUNCH(blocked_to_nchw_kernel, total, dim3(blocks_for(total)), s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int maxpool2_dispatch(const isr_pool_desc* d, int backward, hipStream_t s) {
     const size_t total = (size_t)d->n * d->hao * d->wao * (d->c / 8);
-    if (backward) hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, s, *d);
-    else hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, s, *d);
+    if (backward) ISR_IDX_LAUNCH(maxpool2_bwd_kernel, total, dim3(blocks_for(total)), s, *d);
+    else ISR_IDX_LAUNCH(maxpool2_fwd_kernel, total, dim3(blocks_for(total)), s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -376,11 +392,12 @@ __global__ void bn_finalize_kernel(isr_bn_desc d) {
 }
 
 // y = ((act(a*z + b)) * s1 + r1) * s2 + r2;  a = gamma*invstd, b = beta - mean*a
+template <typename I>
 __global__ __launch_bounds__(256) void bn_apply_kernel(isr_bn_desc d) {
     const int cg = d.c / 8;
-    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        size_t r = i;
+    const I total = (I)((size_t)d.n * d.ha * d.wa * cg);
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+        I r = i;
         const int half = r % 2; r /= 2;
         const int x = r % d.wa; r /= d.wa;
         const int y = r % d.ha; r /= d.ha;
@@ -418,9 +435,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(isr_bn_desc d) {
 }
 
 // dz = gscale * a * (g - sum(g)/N - xhat * sum(g*xhat)/N), in place over y; dgamma/dbeta
+template <typename I>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(isr_bn_desc d) {
     const int cg = d.c / 8;
-    const size_t total = (size_t)d.n * d.ha * d.wa * cg;
+    const I total = (I)((size_t)d.n * d.ha * d.wa * cg);
     const double cnt = (double)d.n * d.h * d.w;
     if (blockIdx.x == 0) {
         for (int c = threadIdx.x; c < d.c; c += blockDim.x) {
@@ -428,8 +446,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(isr_bn_desc d) {
             if (d.dbeta) d.dbeta[c] = (float)(d.acc[c]) * d.gscale;
         }
     }
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        size_t r = i;
+    for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+        I r = i;
         const int half = r % 2; r /= 2;
         const int x = r % d.wa; r /= d.wa;
         const int y = r % d.ha; r /= d.ha;
@@ -460,9 +478,9 @@ int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s) {
     switch (op) {
         case 0: hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(red_blocks), dim3(256), 0, s, *d); break;
         case 1: hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(256), 0, s, *d); break;
-        case 2: hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks), dim3(256), 0, s, *d); break;
+        case 2: ISR_IDX_LAUNCH(bn_apply_kernel, total, dim3(ew_blocks), s, *d); break;
         case 3: hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(red_blocks), dim3(256), 0, s, *d); break;
-        case 4: hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks), dim3(256), 0, s, *d); break;
+        case 4: ISR_IDX_LAUNCH(bn_bwd_apply_kernel, total, dim3(ew_blocks), s, *d); break;
         default: return -2;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
