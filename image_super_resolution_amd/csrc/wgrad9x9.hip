@@ -198,24 +198,26 @@ __global__ __launch_bounds__(C::NT) void wgrad9x9_kernel(W9Args a) {
 
 // dW in the reference OIHW layout: tail [3][64][9][9] (co = p, ci = q), head [64][3][9][9] (co = q, ci = p)
 __global__ void wgrad9_reduce_kernel(W9Args a) {
+    // Threads walk the partial-sum layout [split][ky][r = p*9 + kx (32)][q (64)] in order,
+    // so every split's read is coalesced; the OIHW output is written scattered (once).
     const isr_wgrad9_desc& d = a.d;
-    const size_t per = (size_t)9 * 32 * 64;
-    const int total = 3 * 64 * 81 + (d.db ? (d.head ? 64 : 3) : 0);
-    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-        if (idx < 3 * 64 * 81) {
-            // idx enumerates the output in OIHW order
-            const int kx = idx % 9, ky = (idx / 9) % 9;
-            int p, q;
-            if (d.head) { p = (idx / 81) % 3; q = idx / 243; }   // [q][p][ky][kx]
-            else { q = (idx / 81) % 64; p = idx / (81 * 64); }   // [p][q][ky][kx]
-            const size_t o = ((size_t)ky * 32 + p * 9 + kx) * 64 + q;
+    const int per = 9 * 32 * 64;
+    const int total = per + (d.db ? 64 : 0);
+    for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+        if (o < per) {
+            const int q = o & 63, r = (o >> 6) & 31, ky = o >> 11;
+            if (r >= 27) continue;
+            const int p = r / 9, kx = r - 9 * (r / 9);
             float s = 0.f;
-            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[sp * per + o];
+            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[(size_t)sp * per + o];
+            const int idx = d.head ? ((q * 3 + p) * 9 + ky) * 9 + kx   // dw [64][3][9][9]
+                                   : ((p * 64 + q) * 9 + ky) * 9 + kx; // dw [3][64][9][9]
             d.dw[idx] = s * d.scale;
         } else {
-            const int c = idx - 3 * 64 * 81;
+            const int c = o - per;
+            if (c >= (d.head ? 64 : 3)) continue;
             float s = 0.f;
-            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[a.splits * per + (size_t)sp * 64 + c];
+            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[(size_t)a.splits * per + (size_t)sp * 64 + c];
             d.db[c] = s * d.scale;
         }
     }
@@ -243,7 +245,7 @@ static int launch_w9(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStr
     }
     hipLaunchKernelGGL(kern, dim3(a.splits), dim3(C::NT), C::LDS, s, a);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(wgrad9_reduce_kernel, dim3(64), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(wgrad9_reduce_kernel, dim3((9 * 32 * 64 + 64 + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
