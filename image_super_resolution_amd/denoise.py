@@ -380,15 +380,8 @@ class _DenoiseFn(torch.autograd.Function):
         plan.busy = False
         out = [grads.get(id(p)) for p in plan.params()]
         if plan.grad_group is not None:  # data parallel: one flat RCCL all-reduce (mean), as DDP
-            import torch.distributed as dist
-            grp = None if plan.grad_group is True else plan.grad_group
-            flat = torch.cat([g.reshape(-1) for g in out])
-            dist.all_reduce(flat, group=grp)
-            flat.div_(dist.get_world_size(grp))
-            off = 0
-            for i, g in enumerate(out):
-                out[i] = flat[off:off + g.numel()].view_as(g)
-                off += g.numel()
+            from .train_engine import allreduce_mean
+            out = allreduce_mean(out, None if plan.grad_group is True else plan.grad_group)
         return (None, None, *out)
 
 

@@ -448,17 +448,26 @@ def enable_grad_allreduce(gen: nn.Module, group=True) -> None:
     gen.__dict__["_isr_grad_group"] = group
 
 
+def allreduce_mean(tensors: list, group=None) -> list:
+    """Mean of `tensors` over the process group as ONE flat all-reduce (RCCL on the
+    GPU, gloo in the CPU tests) — DDP's averaging with a single bucket.  Returns views
+    of the reduced flat buffer, one per input tensor."""
+    import torch.distributed as dist
+    if not tensors:
+        return []
+    flat = torch.cat([t.reshape(-1) for t in tensors])
+    dist.all_reduce(flat, group=group)
+    flat.div_(dist.get_world_size(group))
+    out, off = [], 0
+    for t in tensors:
+        out.append(flat[off:off + t.numel()].view_as(t))
+        off += t.numel()
+    return out
+
+
 def allreduce_grads(params, group=None) -> None:
     """Mean of .grad over the group for modules trained outside the HIP plan
     (the discriminator): one flat all-reduce."""
-    import torch.distributed as dist
     grads = [p.grad for p in params if p.grad is not None]
-    if not grads:
-        return
-    flat = torch.cat([g.reshape(-1) for g in grads])
-    dist.all_reduce(flat, group=group)
-    flat.div_(dist.get_world_size(group))
-    off = 0
-    for g in grads:
-        g.copy_(flat[off:off + g.numel()].view_as(g))
-        off += g.numel()
+    for g, r in zip(grads, allreduce_mean(grads, group)):
+        g.copy_(r)

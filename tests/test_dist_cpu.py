@@ -49,3 +49,33 @@ def test_allreduce_grads_matches_full_batch_mean():
     for r in (0, 1):
         for g, p in zip(res[r], m.parameters()):
             torch.testing.assert_close(g, p.grad)
+
+
+def _mean_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from image_super_resolution_amd.train_engine import allreduce_mean
+        ts = [torch.full((3, 2), float(rank + 1)), torch.arange(4.0) * (rank + 1), torch.tensor([float(rank)])]
+        q.put((rank, [t.clone() for t in allreduce_mean(ts)]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_mean_flat_bucket():
+    """The flat one-bucket mean used by the Denoise training plan (denoise._DenoiseFn)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_mean_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        a, b, c = res[r]
+        torch.testing.assert_close(a, torch.full((3, 2), 1.5))
+        torch.testing.assert_close(b, torch.arange(4.0) * 1.5)
+        torch.testing.assert_close(c, torch.tensor([0.5]))
