@@ -197,29 +197,37 @@ __global__ __launch_bounds__(C::NT) void wgrad9x9_kernel(W9Args a) {
 }
 
 // dW in the reference OIHW layout: tail [3][64][9][9] (co = p, ci = q), head [64][3][9][9] (co = q, ci = p)
-__global__ void wgrad9_reduce_kernel(W9Args a) {
-    // Threads walk the partial-sum layout [split][ky][r = p*9 + kx (32)][q (64)] in order,
-    // so every split's read is coalesced; the OIHW output is written scattered (once).
+__global__ __launch_bounds__(256) void wgrad9_reduce_kernel(W9Args a) {
+    // A block owns 64 consecutive entries of the partial-sum layout
+    // [split][ky][r = p*9 + kx (32)][q (64)] (+ the bias partials after it); its 4 waves
+    // take every 4th split, each wave reading 64 consecutive floats (256 B) per split,
+    // and the 4 shares meet in LDS.  The OIHW output is written scattered, once.
+    __shared__ float red[4][64];
     const isr_wgrad9_desc& d = a.d;
     const int per = 9 * 32 * 64;
-    const int total = per + (d.db ? 64 : 0);
-    for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
-        if (o < per) {
-            const int q = o & 63, r = (o >> 6) & 31, ky = o >> 11;
-            if (r >= 27) continue;
-            const int p = r / 9, kx = r - 9 * (r / 9);
-            float s = 0.f;
-            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[(size_t)sp * per + o];
-            const int idx = d.head ? ((q * 3 + p) * 9 + ky) * 9 + kx   // dw [64][3][9][9]
-                                   : ((p * 64 + q) * 9 + ky) * 9 + kx; // dw [3][64][9][9]
-            d.dw[idx] = s * d.scale;
-        } else {
-            const int c = o - per;
-            if (c >= (d.head ? 64 : 3)) continue;
-            float s = 0.f;
-            for (int sp = 0; sp < a.splits; ++sp) s += a.ws[(size_t)a.splits * per + (size_t)sp * 64 + c];
-            d.db[c] = s * d.scale;
-        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int o = blockIdx.x * 64 + lane;
+    const bool bias = o >= per;
+    const int c = o - per;
+    float s = 0.f;
+    if (!bias || (d.db && c < 64)) {
+        const float* src = bias ? a.ws + (size_t)a.splits * per + c : a.ws + o;
+        const size_t stride = bias ? 64 : per;
+        for (int sp = wave; sp < a.splits; sp += 4) s += src[(size_t)sp * stride];
+    }
+    red[wave][lane] = s;
+    __syncthreads();
+    if (wave != 0) return;
+    s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (!bias) {
+        const int q = o & 63, r = (o >> 6) & 31, ky = o >> 11;
+        if (r >= 27) return;
+        const int p = r / 9, kx = r - 9 * (r / 9);
+        const int idx = d.head ? ((q * 3 + p) * 9 + ky) * 9 + kx   // dw [64][3][9][9]
+                               : ((p * 64 + q) * 9 + ky) * 9 + kx; // dw [3][64][9][9]
+        d.dw[idx] = s * d.scale;
+    } else if (d.db && c < (d.head ? 64 : 3)) {
+        d.db[c] = s * d.scale;
     }
 }
 
@@ -245,7 +253,7 @@ static int launch_w9(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStr
     }
     hipLaunchKernelGGL(kern, dim3(a.splits), dim3(C::NT), C::LDS, s, a);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(wgrad9_reduce_kernel, dim3((9 * 32 * 64 + 64 + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(wgrad9_reduce_kernel, dim3((9 * 32 * 64 + 64) / 64), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
