@@ -554,6 +554,8 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 21: return launch3x3<C3<8, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // 32x32 tile, 8 rows per wave (1 block/CU)
             case 22: return launch3x3<C3<8, 2, 1, 16, 2, 0, 0, 2>>(d, s);  // 16x32 tile, 2 waves x 8 rows
             case 23: return launch3x3<C3<2, 8, 1, 16, 2, 0, 0, 2>>(d, s);  // 16x32 tile, 8 waves x 2 rows
+            case 24: return launch3x3<C3<2, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // 8x32 tile, double buffer, interleaved
+            case 25: return launch3x3<C3<2, 4, 1, 16, 3, 0, 0, 2>>(d, s);  // 8x32 tile, 3-deep ring, interleaved
         }
         return -2;
     }
@@ -587,6 +589,8 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
                                       : launch3x3<C3<2, 4, 2, 32, 2, 0, 0, 2>>(d, s);
         case 20: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 64>>(d, s)  // DVFS probe (16x16x32)
                                       : launch3x3<C3<4, 4, 2, 16, 2, 0, 64>>(d, s);
+        case 24: return d->cin == 192 ? launch3x3<C3<2, 4, 2, 16, 2, 192, 0, 2>>(d, s)  // 8x32 tile, interleaved
+                                      : launch3x3<C3<2, 4, 2, 16, 2, 0, 0, 2>>(d, s);
     }
     return -2;
 }

@@ -4,7 +4,8 @@ S sub-batches on S streams, later sub-batches staggered by a spin kernel, vs the
 single-stream plan.  Interleaved rounds in one process; outputs must be identical.
 
 usage: python tools/ab_split.py --configs "1,2:0,2:10,2:20,4:0" [--rounds 7]
-  "S:stagger_us"; "1" = the single-stream GeneratorPlan.
+  "S:stagger_us[:GxWy]"; "1" = the single-stream GeneratorPlan; GxWy = isr_conv3x3_fwd_variant
+  ids for the growth (cout 32) and wide (cout 64/256) convs under the split plan.
 """
 from __future__ import annotations
 
@@ -41,9 +42,15 @@ def main():
         if c == "1":
             plans[c] = engine.GeneratorPlan(gw, args.batch, args.lr_size, args.lr_size, dev, False, False, mean, std)
         else:
-            s, st = c.split(":")
+            parts = c.split(":")
+            s, st = parts[0], parts[1]
+            var = None
+            if len(parts) > 2:  # conv variants "GxWy": x for the cout-32 growth convs, y for cout-64/256
+                g = int(parts[2][1:parts[2].index("W")])
+                w = int(parts[2][parts[2].index("W") + 1:])
+                var = {("conv3x3", "*", 32): g, ("conv3x3", "*", 64): w, ("conv3x3", "*", 256): w}
             plans[c] = engine.SplitGeneratorPlan(gw, args.batch, args.lr_size, args.lr_size, dev, False, False,
-                                                 mean, std, splits=int(s), stagger_us=float(st))
+                                                 mean, std, splits=int(s), stagger_us=float(st), variants=var)
     out = torch.empty(plans[names[0]].out_shape, device=dev)
     ref = None
     for c in names:
