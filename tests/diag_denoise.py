@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-parameter gradient error of the libisr Denoise backward vs fp32 autograd
-through the oracle (diagnostic for tests/test_gpu_denoise.py)."""
+through the oracle (diagnostic for tests/test_gpu_denoise.py; lives under tests/
+because only tests may import oracle/).  usage: python tests/diag_denoise.py"""
 import sys
 from pathlib import Path
 
