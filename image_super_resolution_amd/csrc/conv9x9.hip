@@ -268,6 +268,128 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
     }
 }
 
+// ---- 8-row tail (variant 3): the per-tile kernel with 8 output rows per block and one
+// 32-channel halo chunk resident at a time (chunk 1 refills chunk 0's slot after a
+// barrier), so LDS is 76 KB and two blocks share a CU: one block's halo fetch runs
+// beside the other's MFMAs.  Same MFMA order and ky-sum order as tail9x9_kernel.
+namespace tail8 {
+constexpr int TH = 8, TW = 32, WM = 4;
+constexpr int TR = TH + 8;                    // 16 input rows
+constexpr int RT = TR / WM;                   // 4 input rows per wave
+constexpr int HC = TW + 8;                    // 40 halo cols
+constexpr int HIPL = TR * HC / 32;            // 20 glds per 16-channel plane
+constexpr int HALO_INSTR = 2 * HIPL;          // 40 per 32-channel chunk
+constexpr int HALO_BYTES = HALO_INSTR * 1024; // 40960
+constexpr int W_BYTES = tail::W_BYTES;        // 36864
+constexpr int W_INSTR = W_BYTES / 1024;       // 36
+constexpr int TS = 33;
+constexpr int T_BYTES = TR * 32 * TS * 4;     // 67584
+constexpr int P1 = HALO_BYTES + W_BYTES;      // 77824
+constexpr int LDS = P1 > T_BYTES ? P1 : T_BYTES;
+static_assert(HALO_INSTR % WM == 0 && W_INSTR % WM == 0, "even glds split");
+static_assert(TR * HC % 32 == 0, "");
+static_assert(2 * LDS <= 163840, "two blocks per CU");
+}  // namespace tail8
+
+__global__ __launch_bounds__(256, 2) void tail9x9_k8_kernel(isr_tail_desc d) {
+    using namespace tail8;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int img = blockIdx.z;
+    const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
+    const int wave = wave_id();
+    const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+
+    const char* xbase = view_at(d.x, img, y0 - 4, x0 - 4, 0);
+    const size_t pstride = plane_bytes(d.x);
+    const int xrow = d.x.wp * 32;
+    char* halo = smem;
+    char* wl = smem + HALO_BYTES;
+
+    f32x16 acc[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
+
+    auto load_halo = [&](int chunk) {
+        for (int j = wave; j < HALO_INSTR; j += WM) {
+            const int kp = j / HIPL;
+            const int u = (j - kp * HIPL) * 64 + lane;
+            const int q = u >> 1;
+            const int row = q / HC, col = q - row * HC;
+            const int c = (u & 1) ^ ((q >> 3) & 1);
+            glds16(xbase + (size_t)(chunk * 2 + kp) * pstride + row * xrow + col * 32 + c * 16, halo + j * 1024);
+        }
+    };
+    for (int j = wave; j < W_INSTR; j += WM)
+        glds16((const char*)d.wpack + j * 1024 + lane * 16, wl + j * 1024);
+    load_halo(0);
+
+#pragma unroll
+    for (int chunk = 0; chunk < 2; ++chunk) {
+        wait_vm0();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int kx = 0; kx < 9; ++kx) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int n = l31;
+                const bf16x8 b = lds_read16(wl + ((((kx * 2 + chunk) * 2 + ks) * 32 + n) * 2 + (hh ^ ((n >> 3) & 1))) * 16);
+                const char* hp = halo + ks * HIPL * 1024;
+#pragma unroll
+                for (int t = 0; t < RT; ++t) {
+                    const int q = (wave * RT + t) * HC + kx + l31;
+                    acc[t] = mfma32(lds_read16(hp + halo_unit2(q, hh) * 16), b, acc[t]);
+                }
+            }
+        }
+        if (chunk == 0) {
+            __syncthreads();  // every wave is done with chunk 0's halo before it is overwritten
+            load_halo(1);
+        }
+    }
+    __syncthreads();
+
+    float* T = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int px = (g & 3) + 8 * (g >> 2) + 4 * hh;
+            T[((wave * RT + t) * 32 + px) * TS + l31] = acc[t][g];
+        }
+    __syncthreads();
+
+    const size_t plane = (size_t)d.h * d.w;
+    for (int item = threadIdx.x; item < TH * TW; item += 256) {
+        const int yr = item >> 5, px = item & 31;
+        const int yy = y0 + yr, xx = x0 + px;
+        float s[3];
+#pragma unroll
+        for (int co = 0; co < 3; ++co) s[co] = d.bias ? d.bias[co] : 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 9; ++ky) {
+            const float* tp = T + ((yr + ky) * 32 + px) * TS + ky * 3;
+#pragma unroll
+            for (int co = 0; co < 3; ++co) s[co] += tp[co];
+        }
+        if (yy < d.h && xx < d.w) {
+            const size_t o = (size_t)img * 3 * plane + (size_t)yy * d.w + xx;
+#pragma unroll
+            for (int co = 0; co < 3; ++co) {
+                const float t = tanhf(s[co]);
+                if (d.y_u8) {
+                    const float q = rintf((t + 1.f) / 2.f * 255.f);
+                    ((uint8_t*)d.y)[o + co * plane] = (uint8_t)fminf(fmaxf(q, 0.f), 255.f);
+                } else {
+                    ((float*)d.y)[o + co * plane] = t;
+                }
+            }
+        }
+    }
+}
+
 // ---- persistent tail (variant 2, not production: see tail9x9_fwd_variant): one block per CU walks its tiles, 16-channel halo planes
 // stream through a 3-deep LDS ring (the next tile's first planes load while this
 // tile finishes), weights stay resident, and the ky-sum goes through small per-wave
@@ -498,10 +620,10 @@ int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s) {
 }
 
 int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
-    // production = variant 1, the one-tile-per-block kernel (≈375 us at 16 x 512²): the
-    // persistent variant 2 measures 515 us (LDS-atomic slices: 990 us; its main loop alone
-    // ≈330 us at one wave per SIMD; tools/tune_tail.py)
-    if (variant == 0) variant = 1;
+    // production = variant 3, the 8-row tile with two blocks per CU (381 vs 401 us for the
+    // 16-row one-block-per-CU variant 1 at 16 x 512², bit-identical outputs); the persistent
+    // variant 2 measures 515 us (LDS-atomic slices: 990 us; tools/tune_tail.py)
+    if (variant == 0) variant = 3;
     if (variant == 2 || (variant >= 10 && variant <= 17)) {  // persistent
         static int cus = 0;
         if (!cus) {
@@ -526,6 +648,17 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             case 13: return go(tail9x9_pkernel<8>);
             default: return go(tail9x9_pkernel<0>);
         }
+    }
+    if (variant == 3) {
+        static bool attr8 = false;
+        if (!attr8) {
+            (void)hipFuncSetAttribute((const void*)tail9x9_k8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      tail8::LDS);
+            attr8 = true;
+        }
+        dim3 grid8(d->wa / tail8::TW, d->ha / tail8::TH, d->n);
+        hipLaunchKernelGGL(tail9x9_k8_kernel, grid8, dim3(256), tail8::LDS, s, *d);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (variant != 1) return -2;
     static bool attr = false;

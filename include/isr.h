@@ -310,7 +310,7 @@ int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s);
 int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_t s);
 int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s);
 int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);
-/* Tuning / A-B entry point: 0 = production (= 1), 1 = one tile per block, 2 = persistent
+/* Tuning / A-B entry point: 0 = production (= 3), 1 = one tile per block, 3 = one 8-row tile per block (76 KB LDS, 2 blocks / CU), 2 = persistent
  * (one block per CU, streamed halo ring; slower: its partial-sum epilogue dominates).
  * Same descriptor rules as isr_tail9x9_fwd. */
 int isr_tail9x9_fwd_variant(const isr_tail_desc* d, int32_t variant, isr_stream_t s);

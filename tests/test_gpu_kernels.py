@@ -184,7 +184,12 @@ def test_tail9x9_persistent_vs_per_tile(n, h, w):
             ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(d), v, ops._stream()), "tail variant")
             torch.cuda.synchronize()
             outs.setdefault((dt, v), []).append(o)
+        o8 = torch.empty(n, 3, h, w, device=DEV, dtype=dt)  # 8-row, two-blocks-per-CU variant: same sums
+        d8 = ops.tail9x9_desc(xb, wp, b, o8)
+        ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(d8), 3, ops._stream()), "tail variant 3")
+        torch.cuda.synchronize()
         a, p0, p1 = outs[(dt, 1)][0], outs[(dt, 2)][0], outs[(dt, 2)][1]
+        assert torch.equal(o8, a)
         assert torch.equal(p0, p1)
         if dt == torch.float32:
             assert (a - p0).abs().max().item() < 1e-5
