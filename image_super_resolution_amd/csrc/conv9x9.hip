@@ -23,7 +23,7 @@ constexpr int R = 4, WM = 4, NF = 2, TH = R * WM, TW = 32, CT = NF * 32;
 constexpr int HR = TH + 8, HC = 44; // halo cols: 32 + 8, padded so tap groups 9..11 stay in range
 constexpr int HALO_BYTES = HR * HC * 8;
 constexpr int EPS = CT + 4;
-constexpr int EP_BYTES = WM * R * 32 * EPS * 4;
+constexpr int EP_BYTES = WM * 32 * EPS * 4;  // one output row per wave at a time
 constexpr int LDS = EP_BYTES > HALO_BYTES ? EP_BYTES : HALO_BYTES;
 }  // namespace head
 
@@ -99,34 +99,37 @@ __global__ __launch_bounds__(256) void head9x9_kernel(isr_head_desc d) {
     }
     __syncthreads();
 
-    float* ep = reinterpret_cast<float*>(smem) + wave * (R * 32 * EPS);
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int g = 0; g < 16; ++g) {
-                const int px = (g & 3) + 8 * (g >> 2) + 4 * hh;
-                ep[(r * 32 + px) * EPS + f * 32 + l31] = acc[r][f][g];
-            }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
-
+    // epilogue one output row per wave at a time through a wave-private 32 x EPS float
+    // image (35 KB for the block instead of 139 KB: more than one block per CU)
+    float* ep = reinterpret_cast<float*>(smem) + wave * (32 * EPS);
     Epi e;
     e.bias = d.bias; e.slope = d.slope; e.s1 = 1.f; e.s2 = 1.f;
     e.y = d.y; e.y2 = d.y2; e.r1.data = nullptr; e.r2.data = nullptr; e.h = d.h; e.w = d.w;
     e.m = d.m; e.mslope = d.mslope;
     constexpr int CG = CT / 8;
-#pragma unroll 4
-    for (int it = 0; it < R * CT / 16; ++it) {
-        const int jj = lane + 64 * it;
-        const int cg = jj % CG, p = jj / CG;
-        const int r = p >> 5, px = p & 31;
-        float v[8];
-        const float* src = ep + (r * 32 + px) * EPS + cg * 8;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = src[k];
-        epi_plain8(e, v, img, y0 + wave * R + r, x0 + px, cg * 8);
+    for (int r = 0; r < R; ++r) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // previous row's image reads are complete
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int px = (g & 3) + 8 * (g >> 2) + 4 * hh;
+                ep[px * EPS + f * 32 + l31] = acc[r][f][g];
+            }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < CT / 16; ++it) {
+            const int jj = lane + 64 * it;
+            const int cg = jj % CG, px = jj / CG;
+            float v[8];
+            const float* src = ep + px * EPS + cg * 8;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = src[k];
+            epi_plain8(e, v, img, y0 + wave * R + r, x0 + px, cg * 8);
+        }
     }
 }
 
