@@ -9,25 +9,31 @@ engine.SplitGeneratorPlan; --streams 1 for the single-stream plan).  Multi-GPU: 
 rank runs its own 16 tiles (tiles are independent: weak scaling, no
 collective on the data path; only the timing uses a MAX all-reduce).
 
-Prints one JSON line (rank 0).  Extra fields:
-  roofline      — dominant kernel (conv3x3 192→64, 48 launches per forward):
-                  timed in isolation on a single-stream full-batch plan (same
-                  kernel, full-batch grid; under the split plan two half-batch
-                  launches share the CUs, so their durations are not their own):
-                  its 48 launches of one forward replayed back to back on the
-                  launch stream between one pair of HIP events (5 rounds, after
-                  the timed region), so the per-launch average matches the
-                  rocprofv3 kernel-trace average of the same command; the
-                  in-network bracketed average (events around each launch of 3
-                  untimed forwards after the timed region: event records inside
-                  the timed loop would cost ~4 % of a step) is reported beside it.  achieved =
-                  algorithmic FLOPs per launch / avg launch time, against the
-                  2.5 PFLOP/s dense bf16 MFMA peak.
-                  traffic = PMC HBM bytes per launch from
-                  profiles/<round>_pmc_traffic.json (rocprofv3 --pmc pass of this
-                  command, corrected per MI355X_MICROARCH.md), or null.
+Prints one JSON line (rank 0).  The timed steps replay the forward as one HIP
+graph (engine.GraphedPlan; --no-graph for the eager ctypes launch loop, whose
+~15 us of host time per launch would otherwise bound the step).  Extra fields:
+  roofline      — the dominant kernel: the RDB growth conv (conv3x3_fwd with a
+                  32-cout tile, 4 x 48 launches per forward, the largest share
+                  of the step), against the HBM bound.  Algorithmic bytes per
+                  launch = (cin + 32) channels x 2 B x N*H*W (input read once,
+                  output written once; weights < 0.1 %), averaged over the four
+                  growth shapes (cin 64/96/128/160).  Its 192 launches of one
+                  forward are replayed back to back on the launch stream between
+                  one pair of HIP events (5 rounds, median; single-stream
+                  full-batch plan), so the per-launch average matches rocprofv3's
+                  kernel trace of the same command.  traffic = PMC HBM bytes per
+                  launch of that kernel from profiles/<round>_pmc_traffic.json
+                  (rocprofv3 --pmc, corrected per MI355X_MICROARCH.md), or null.
+  roofline_kernels — the same measurement for both conv templates, each against
+                  its own bound: growth (HBM) and the RDB final conv 192->64
+                  (MFMA, 2*9*192*64 FLOP per output pixel).
+  model_roofline — SURVEY.md §8d: max(F / P_mfma, B / BW_hbm) / t_step for the
+                  whole forward (F = 410.9 GFLOP and B = 1.403 GB bf16 per 128²
+                  tile at layer granularity).
   cpu_baseline  — the parity-verified CPU restatement (oracle/ref_cpu.py, torch
-                  fp32) timed on this host on a bounded sample (batch-1 tiles).
+                  fp32) on this host's CPUs available to the process (affinity,
+                  capped by the cgroup CPU quota; the count is stated), batch 1
+                  and batch 16 (`value` = batch 16, the GPU workload's shape).
   parity        — PSNR of the GPU output vs that CPU reference on the same
                   tile, and the |ΔPSNR| against the synthetic HR target.
 """
@@ -50,7 +56,11 @@ sys.path.insert(0, str(ROOT))
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense, MI355X_MICROARCH.md chip table
 HBM_PEAK_GBS = 8000.0
-DOMINANT = ("conv3x3", 192, 64)
+GROWTH = tuple(("conv3x3", 64 + 32 * k, 32) for k in range(4))  # RDB growth convs (32-cout tile)
+FINAL = (("conv3x3", 192, 64),)                                  # RDB final conv
+# SURVEY.md §8d, per 128x128 LR tile of ResNet(16, x4): FLOPs and layer-granularity bf16 bytes
+TILE_FLOP = 410.9e9
+TILE_BYTES = 1.403e9
 
 
 def parse():
@@ -64,22 +74,54 @@ def parse():
     ap.add_argument("--scale", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r01")
+    ap.add_argument("--round", default="r02")
+    ap.add_argument("--no-graph", action="store_true", help="eager launch loop instead of the HIP graph")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N>1 (nccl = RCCL)")
     ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams the batch is split over (default engine.DEFAULT_STREAMS)")
     return ap.parse_args()
 
 
-def load_traffic(round_tag: str):
+def load_traffic(round_tag: str) -> dict:
+    """{family: PMC HBM bytes per launch} from profiles/<round>_pmc_traffic.json."""
     p = ROOT / "profiles" / f"{round_tag}_pmc_traffic.json"
     if not p.exists():
-        return None
+        return {}
     try:
         d = json.loads(p.read_text())
-        return d.get("hbm_bytes_per_launch")
+        return {k: v.get("hbm_bytes_per_launch") for k, v in d.get("families", {}).items()}
     except Exception:
-        return None
+        return {}
+
+
+def cpu_cores() -> dict:
+    """CPUs this process may actually use: affinity, capped by the cgroup v2 quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    return {"use": min(aff, quota) if quota else aff, "os_cpu_count": os.cpu_count(), "affinity": aff,
+            "cgroup_quota": quota}
+
+
+def time_family(plan, tags, stream, sp, rounds=5):
+    """Median per-launch ms of `plan`'s launches tagged in `tags`, replayed back to
+    back in forward order between one pair of HIP events on the launch stream."""
+    launches = [(fn, d, tag) for fn, d, tag, var in plan.launches if tag in tags and var is None]
+    res = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for fn, d, _ in launches:
+            fn(ctypes.byref(d), sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        res.append(e0.elapsed_time(e1) / len(launches))
+    return statistics.median(res), [t for _, _, t in launches]
 
 
 def main():
@@ -115,26 +157,21 @@ def main():
     plan = engine.get_plan(gw, x, False, mean, std, streams=args.streams)
     n_streams = len(plan.streams) if isinstance(plan, engine.SplitGeneratorPlan) else 1
     out = torch.empty(plan.out_shape, dtype=plan.out_dtype, device=dev)
+    if args.no_graph:
+        step = lambda: plan.run(x, out)  # noqa: E731
+    else:
+        step = engine.GraphedPlan(plan, x, out).run
 
     for _ in range(args.warmup):
-        plan.run(x, out)
+        step()
     torch.cuda.synchronize()
-
-    pairs = []
-
-    def around(tag):
-        if tag == DOMINANT:
-            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            pairs.append(e)
-            return e
-        return None
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        plan.run(x, out)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -147,35 +184,40 @@ def main():
     ms = elapsed / args.steps * 1e3
     hr_px = n * (hw * S) * (hw * S)
     mpix_s = world * hr_px * args.steps / elapsed / 1e6
-    # The dominant kernel is timed in isolation: the full batch on ONE stream (with the
-    # split plan two half-batch launches share the CUs, so a launch's duration is not
-    # its own).  First its launches inside the network, event-bracketed, in untimed
-    # forwards of their own (96 event records cost ~4 % of a step, so they stay out of
-    # the timed loop) ...
+    # Per-kernel roofline: each conv template's launches of one forward replayed back to
+    # back on a single-stream full-batch plan (under the split plan two half-batch
+    # launches share the CUs, so a launch's duration is not its own); after the timed region.
     iso = plan if n_streams == 1 else engine.GeneratorPlan(gw, n, hw, hw, dev, False, False, mean, std)
-    for _ in range(3):
-        iso.run(x, out, around=around)
+    iso.run(x, out)
     torch.cuda.synchronize()
-    in_net_ms = statistics.mean(a.elapsed_time(b) for a, b in pairs)
-    # ... then back to back (per-launch time without the event packets interleaved
-    # between every launch)
-    dom = [(fn, d) for fn, d, tag, var in iso.launches if tag == DOMINANT and var is None]
-    stream = torch.cuda.current_stream()
-    sp = ops._stream()
-    rounds = []
-    for _ in range(5):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for fn, d in dom:
-            fn(ctypes.byref(d), sp)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        rounds.append(e0.elapsed_time(e1) / len(dom))
-    kernel_ms = statistics.median(rounds)
-    flops_launch = 2.0 * n * hw * hw * 9 * DOMINANT[1] * DOMINANT[2]
-    achieved = flops_launch / (kernel_ms * 1e-3) / 1e12
-    model_flops = engine.generator_flops(hw, hw, args.blocks, S // 2) * n
+    stream, sp = torch.cuda.current_stream(), ops._stream()
+    npx = n * hw * hw
     traffic = load_traffic(args.round)
+    kernels = {}
+    g_ms, g_tags = time_family(iso, GROWTH, stream, sp)
+    g_bytes = statistics.mean((t[1] + t[2]) * 2 * npx for t in g_tags)
+    g_flops = statistics.mean(2.0 * 9 * t[1] * t[2] * npx for t in g_tags)
+    g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
+    kernels["growth"] = {"bound": "hbm", "kernel": "conv3x3_fwd 32-cout tile (RDB growth convs, cin 64/96/128/160)",
+                         "achieved": round(g_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(g_gbs / HBM_PEAK_GBS, 4), "traffic": traffic.get("growth"),
+                         "bytes_per_launch": g_bytes, "avg_launch_ms": round(g_ms, 5),
+                         "launches_per_step": len(g_tags),
+                         "mfma_frac": round(g_flops / (g_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4)}
+    f_ms, f_tags = time_family(iso, FINAL, stream, sp)
+    f_flops = 2.0 * npx * 9 * 192 * 64
+    f_tf = f_flops / (f_ms * 1e-3) / 1e12
+    kernels["final"] = {"bound": "mfma", "kernel": "conv3x3_fwd 192->64 (RDB final conv)",
+                        "achieved": round(f_tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(f_tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic.get("final"),
+                        "flops_per_launch": f_flops, "avg_launch_ms": round(f_ms, 5),
+                        "launches_per_step": len(f_tags)}
+    model_flops = engine.generator_flops(hw, hw, args.blocks, S // 2) * n
+    f_over_p = model_flops / (MFMA_BF16_PEAK_TFLOPS * 1e12) * 1e3
+    b_over_bw = TILE_BYTES * n * (hw * hw) / (128 * 128) / (HBM_PEAK_GBS * 1e9) * 1e3
+    model_roofline = {"F_over_P_ms": round(f_over_p, 4), "B_over_BW_ms": round(b_over_bw, 4),
+                      "frac": round(max(f_over_p, b_over_bw) / ms, 4),
+                      "mfma_frac": round(f_over_p / ms, 4), "hbm_frac": round(b_over_bw / ms, 4)}
 
     result = None
     if rank == 0:
@@ -184,21 +226,30 @@ def main():
         if not args.no_cpu_baseline:
             from oracle import ref_cpu
             torch.set_grad_enabled(False)
+            cores = cpu_cores()
+            torch.set_num_threads(cores["use"])
             x1 = x_cpu[:1]
             ts = []
             ref = None
             t_start = time.perf_counter()
-            while True:
+            while True:  # batch 1: one warm-up + up to 3 timed
                 t1 = time.perf_counter()
                 ref = ref_cpu.generator(sd_cpu, x1, num_blocks=args.blocks, scale=S)
                 ts.append(time.perf_counter() - t1)
-                if len(ts) >= 8 or time.perf_counter() - t_start > args.cpu_seconds:
+                if len(ts) >= 4 or time.perf_counter() - t_start > args.cpu_seconds / 2:
                     break
-            tcpu = statistics.median(ts[1:]) if len(ts) > 1 else ts[0]
-            cpu = {"value": round((hw * S) ** 2 / tcpu / 1e6, 4), "unit": "MPix/s",
-                   "cores": torch.get_num_threads(), "kind": "port",
-                   "sample": f"oracle/ref_cpu.generator fp32, 1 tile {hw}x{hw}->{hw * S}x{hw * S}, "
-                             f"{len(ts)} runs (first = warm-up), median {tcpu:.3f} s/tile"}
+            t_b1 = statistics.median(ts[1:]) if len(ts) > 1 else ts[0]
+            nb = min(n, 16)
+            t1 = time.perf_counter()
+            ref_cpu.generator(sd_cpu, x_cpu[:nb], num_blocks=args.blocks, scale=S)
+            t_b16 = time.perf_counter() - t1
+            cpu = {"value": round(nb * (hw * S) ** 2 / t_b16 / 1e6, 4), "unit": "MPix/s",
+                   "cores": cores["use"], "kind": "port",
+                   "batch1_mpix_s": round((hw * S) ** 2 / t_b1 / 1e6, 4),
+                   "os_cpu_count": cores["os_cpu_count"], "cgroup_quota_cpus": cores["cgroup_quota"],
+                   "sample": f"oracle/ref_cpu.generator fp32 (torch CPU, {cores['use']} threads), "
+                             f"batch {nb} of {hw}x{hw}->{hw * S}x{hw * S}: one run {t_b16:.2f} s; batch 1: "
+                             f"{len(ts)} runs (first = warm-up), median {t_b1:.3f} s/tile"}
             g = out[:1].float().cpu()
             hr1 = hr[:1] * 2 - 1
             parity = {"psnr_gpu_vs_cpu_ref_db": round(ref_cpu.psnr(g, ref), 3),
@@ -221,14 +272,11 @@ def main():
                                    f"{hw}x{hw}->{hw * S}x{hw * S}",
                        "global_batch": n * world, "per_gpu_batch": n, "lr_size": hw, "scale": S,
                        "parallelism": f"dp{world} (independent tile shards)",
-                       "streams_per_gpu": n_streams},
-            "roofline": {"bound": "mfma", "kernel": "conv3x3_fwd 192->64 (RDB final conv)",
-                         "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
-                         "avg_launch_ms": round(kernel_ms, 5), "in_network_avg_launch_ms": round(in_net_ms, 5),
-                         "launches_per_step": len(dom), "flops_per_launch": flops_launch},
-            "model_tflops_per_s": round(model_flops * world / (ms * 1e-3) / 1e12 / world, 2),
-            "model_mfma_frac": round(model_flops / (ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+                       "streams_per_gpu": n_streams, "hip_graph": not args.no_graph},
+            "roofline": kernels["growth"],
+            "roofline_kernels": kernels,
+            "model_roofline": model_roofline,
+            "model_tflops_per_s": round(model_flops / (ms * 1e-3) / 1e12, 2),
             "cpu_baseline": cpu,
             "parity": parity,
         }

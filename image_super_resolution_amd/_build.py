@@ -3,6 +3,10 @@
 No cmake/ninja: one hipcc invocation per .hip file (run in parallel), then a
 link.  The output lands in image_super_resolution_amd/lib/ so it travels with
 the repository snapshot to the GPU box.
+
+`python -m image_super_resolution_amd._build --tuning` builds lib/libisr_tuning.so
+with -DISR_TUNING (adds timing-only ablation variants whose outputs are wrong);
+tools load it with ISR_LIB=<path>.  The production libisr.so never contains them.
 """
 from __future__ import annotations
 
@@ -35,10 +39,12 @@ def _needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    if not force and not _needs_build():
+def build(force: bool = False, verbose: bool = False, tuning: bool = False) -> Path:
+    lib_path = LIBDIR / "libisr_tuning.so" if tuning else LIB
+    if not tuning and not force and not _needs_build():
         return LIB
-    objdir = PKG / "build"
+    objdir = PKG / ("build_tuning" if tuning else "build")
+    flags = FLAGS + (["-DISR_TUNING"] if tuning else [])
     objdir.mkdir(exist_ok=True)
     LIBDIR.mkdir(exist_ok=True)
 
@@ -49,7 +55,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         obj = objdir / (src.stem + ".o")
         if not force and obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, newest_header):
             return obj  # incremental: object newer than its source and every header
-        cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *flags, "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -61,14 +67,14 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(8, len(sources()))) as ex:
         objs = list(ex.map(compile_one, sources()))
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = lib_path.with_suffix(".so.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, tuning="--tuning" in sys.argv))

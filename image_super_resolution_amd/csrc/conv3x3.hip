@@ -498,11 +498,7 @@ static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
     if (d->cout % C::CT || d->cin % C::KC || d->ha % C::TH) return -2;
     if (C::CIN && d->cin != C::CIN) return -2;
     auto kern = conv3x3_fwd_kernel<C>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-        attr = true;
-    }
+    lds_limit((const void*)kern, C::LDS);
     const int blocks = (d->wa / C::TW) * (d->ha / C::TH) * d->n * (d->cout / C::CT);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -533,11 +529,15 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 1: return launch3x3<V_G1>(d, s);
             case 2: return launch3x3<V_G2>(d, s);
             case 3: return launch3x3<V_G3>(d, s);
-            // ablations of V_G1 (timing only)
+#ifdef ISR_TUNING
+            // ablations of V_G0 (timing only, outputs wrong): tuning builds only
             case 4: return launch3x3<C3<4, 4, 1, 16, 2, 0, 1>>(d, s);
             case 5: return launch3x3<C3<4, 4, 1, 16, 2, 0, 2>>(d, s);
             case 6: return launch3x3<C3<4, 4, 1, 16, 2, 0, 4>>(d, s);
             case 7: return launch3x3<C3<4, 4, 1, 16, 2, 0, 3>>(d, s);
+            case 16: return launch3x3<C3<4, 4, 1, 16, 2, 0, 32>>(d, s);  // probe: dx>0 activations by DPP shift
+            case 20: return launch3x3<C3<4, 4, 1, 16, 2, 0, 64>>(d, s);  // DVFS probe: 2x 16x16x32 per 32x32x16
+#endif
             case 8: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 1>>(d, s);  // V_G0, one unit per epilogue pass
             case 9: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 4, 2>>(d, s);  // V_G0, refill split over 2 steps
             case 10: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 4, 3>>(d, s); // V_G0, refill split over 3 steps
@@ -546,11 +546,9 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
             case 13: return launch3x3<C3<2, 4, 1, 16, 2>>(d, s);  // 8x32 tile, double buffer (3 blocks/CU)
             case 14: return launch3x3<C3<4, 4, 1, 16, 2, 0, 8>>(d, s);   // V_G0, second block slot ~0.5 us late
             case 15: return launch3x3<C3<4, 4, 1, 16, 2, 0, 16>>(d, s);  // V_G0, second block slot ~1 us late
-            case 16: return launch3x3<C3<4, 4, 1, 16, 2, 0, 32>>(d, s);  // probe: dx>0 activations by DPP shift
             case 17: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // V_G0, reads interleaved with MFMAs
             case 18: return launch3x3<C3<4, 4, 1, 32, 2, 0, 0, 2>>(d, s);  // KC32 (1 block/CU), interleaved
             case 19: return launch3x3<C3<2, 4, 1, 32, 2, 0, 0, 2>>(d, s);  // 8x32 KC32, interleaved
-            case 20: return launch3x3<C3<4, 4, 1, 16, 2, 0, 64>>(d, s);  // DVFS probe: 2x 16x16x32 per 32x32x16
             case 21: return launch3x3<C3<8, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // 32x32 tile, 8 rows per wave (1 block/CU)
             case 22: return launch3x3<C3<8, 2, 1, 16, 2, 0, 0, 2>>(d, s);  // 16x32 tile, 2 waves x 8 rows
             case 23: return launch3x3<C3<2, 8, 1, 16, 2, 0, 0, 2>>(d, s);  // 16x32 tile, 8 waves x 2 rows
@@ -564,11 +562,17 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
         case 1: return launch3x3<V_W1>(d, s);
         case 2: return launch3x3<V_W2>(d, s);
         case 3: return launch3x3<V_W3>(d, s);
-        // ablations of V_W0 (timing only)
+#ifdef ISR_TUNING
+        // ablations of V_W0 (timing only, outputs wrong): tuning builds only
         case 4: return launch3x3<C3<4, 4, 2, 16, 2, 0, 1>>(d, s);
         case 5: return launch3x3<C3<4, 4, 2, 16, 2, 0, 2>>(d, s);
         case 6: return launch3x3<C3<4, 4, 2, 16, 2, 0, 4>>(d, s);
         case 7: return launch3x3<C3<4, 4, 2, 16, 2, 0, 3>>(d, s);
+        case 16: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 32>>(d, s)  // probe: DPP-shifted dx>0
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 32>>(d, s);
+        case 20: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 64>>(d, s)  // DVFS probe (16x16x32)
+                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 64>>(d, s);
+#endif
         case 8: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 0, 1>>(d, s)  // V_F0 / V_W0, one unit per pass
                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 1>>(d, s);
         case 9: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 0, 4, 2>>(d, s)  // refill split over 2 steps
@@ -581,14 +585,10 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
                                       : launch3x3<C3<4, 4, 2, 16, 2, 0, 8>>(d, s);
         case 15: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 16>>(d, s)  // ~1 us late
                                       : launch3x3<C3<4, 4, 2, 16, 2, 0, 16>>(d, s);
-        case 16: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 32>>(d, s)  // probe: DPP-shifted dx>0
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 32>>(d, s);
         case 17: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 2>>(d, s)  // reads interleaved with MFMAs
                                       : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 2>>(d, s);
         case 18: return d->cin == 192 ? launch3x3<C3<2, 4, 2, 32, 2, 192, 0, 2>>(d, s)  // 8x32 KC32, interleaved
                                       : launch3x3<C3<2, 4, 2, 32, 2, 0, 0, 2>>(d, s);
-        case 20: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 64>>(d, s)  // DVFS probe (16x16x32)
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 64>>(d, s);
         case 24: return d->cin == 192 ? launch3x3<C3<2, 4, 2, 16, 2, 192, 0, 2>>(d, s)  // 8x32 tile, interleaved
                                       : launch3x3<C3<2, 4, 2, 16, 2, 0, 0, 2>>(d, s);
     }

@@ -612,11 +612,7 @@ __global__ void pack_tail_kernel(const float* __restrict__ w, __bf16* __restrict
 
 // ============================== launchers ================================
 int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)head9x9_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, head::LDS);
-        attr = true;
-    }
+    lds_limit((const void*)head9x9_kernel, head::LDS);
     dim3 grid(d->wa / head::TW, d->ha / head::TH, d->n);
     hipLaunchKernelGGL(head9x9_kernel, grid, dim3(256), head::LDS, s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -628,47 +624,30 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
     // variant 2 measures 515 us (LDS-atomic slices: 990 us; tools/tune_tail.py)
     if (variant == 0) variant = 3;
     if (variant == 2 || (variant >= 10 && variant <= 17)) {  // persistent
-        static int cus = 0;
-        if (!cus) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-                cus = 256;
-        }
+        const int cus = cu_count();
         const int ntiles = d->n * (d->ha / tail::TH) * (d->wa / tail::TW);
         const int grid = ntiles < cus ? ntiles : cus;
         auto go = [&](auto kern) {
-            static bool attr = false;
-            if (!attr) {
-                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, tailp::LDS);
-                attr = true;
-            }
+            lds_limit((const void*)kern, tailp::LDS);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), tailp::LDS, s, *d, ntiles);
             return hipGetLastError() == hipSuccess ? 0 : -1;
         };
         switch (variant) {
-            case 12: return go(tail9x9_pkernel<2>);
+#ifdef ISR_TUNING
+            case 12: return go(tail9x9_pkernel<2>);  // timing probes, outputs wrong: tuning builds only
             case 13: return go(tail9x9_pkernel<8>);
+#endif
             default: return go(tail9x9_pkernel<0>);
         }
     }
     if (variant == 3) {
-        static bool attr8 = false;
-        if (!attr8) {
-            (void)hipFuncSetAttribute((const void*)tail9x9_k8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      tail8::LDS);
-            attr8 = true;
-        }
+        lds_limit((const void*)tail9x9_k8_kernel, tail8::LDS);
         dim3 grid8(d->wa / tail8::TW, d->ha / tail8::TH, d->n);
         hipLaunchKernelGGL(tail9x9_k8_kernel, grid8, dim3(256), tail8::LDS, s, *d);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (variant != 1) return -2;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)tail9x9_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, tail::LDS);
-        attr = true;
-    }
+    lds_limit((const void*)tail9x9_kernel, tail::LDS);
     dim3 grid(d->wa / tail::TW, d->ha / tail::TH, d->n);
     hipLaunchKernelGGL(tail9x9_kernel, grid, dim3(256), tail::LDS, s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;

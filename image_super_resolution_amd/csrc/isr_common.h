@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "isr.h"
 
 namespace isr {
@@ -122,6 +126,33 @@ __device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int 
     }
     store8_bf16(view_at(e.y, img, yy, xx, co), v);
     if (e.y2.data) store8_bf16(view_at(e.y2, img, yy, xx, co), v);
+}
+
+// Raise `kern`'s dynamic-LDS limit to `bytes` once per (kernel, device).  The
+// library is called from the Python thread (forward) and from autograd's device
+// thread (backward), and one process may drive several devices, so the
+// bookkeeping is per device and mutex-protected.
+inline void lds_limit(const void* kern, int bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.insert({kern, dev}).second)
+        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+// Compute units of the current device (cached per device).
+inline int cu_count() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static std::mutex mu;
+    static int cache[64] = {0};
+    std::lock_guard<std::mutex> lock(mu);
+    int& c = cache[dev & 63];
+    if (c <= 0 && (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0))
+        c = 256;
+    return c;
 }
 
 }  // namespace isr

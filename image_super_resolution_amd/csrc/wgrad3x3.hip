@@ -352,11 +352,7 @@ static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipS
     if (ws_bytes < ((size_t)a.splits * 9 * d->cout * d->cin + (size_t)a.splits * d->cout) * 4) return -3;
     a.ws = (float*)ws;
     auto kern = wgrad3x3_kernel<C>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-        attr = true;
-    }
+    lds_limit((const void*)kern, C::LDS);
     const int blocks = a.splits * (d->cout / C::CO_T) * (d->cin / C::CI_T);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, a);
     if (hipGetLastError() != hipSuccess) return -1;

@@ -246,11 +246,7 @@ static int launch_w9(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStr
     if (ws_bytes < (size_t)a.splits * (9 * 32 * 64 + 64) * 4) return -3;
     a.ws = (float*)ws;
     auto kern = wgrad9x9_kernel<C>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-        attr = true;
-    }
+    lds_limit((const void*)kern, C::LDS);
     hipLaunchKernelGGL(kern, dim3(a.splits), dim3(C::NT), C::LDS, s, a);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(wgrad9_reduce_kernel, dim3((9 * 32 * 64 + 64) / 64), dim3(256), 0, s, a);

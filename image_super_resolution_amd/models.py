@@ -207,7 +207,8 @@ class _Generator(nn.Module):
         return _isr_free_state(self)
 
     def _packed(self, device) -> engine.GeneratorWeights:
-        key = (str(device),) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
+        key = (str(device), ops.param_write_epoch()) + tuple((t.data_ptr(), t._version)
+                                                             for t in self.state_dict().values())
         cache = self.__dict__.get("_isr_pack")
         if cache is None or cache[0] != key:
             gw = engine.pack_generator(self.state_dict(), enchant=self.enchant, add_rate=self.add_rate,
@@ -336,7 +337,8 @@ class Denoise(nn.Module):
 
     def _packed(self, device):
         from .denoise import pack_denoise
-        key = (str(device),) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
+        key = (str(device), ops.param_write_epoch()) + tuple((t.data_ptr(), t._version)
+                                                             for t in self.state_dict().values())
         cache = self.__dict__.get("_isr_pack")
         if cache is None or cache[0] != key:
             dw = pack_denoise(self.state_dict(), device=device)

@@ -15,6 +15,20 @@ from . import _lib
 from ._lib import IsrConvDesc, IsrConvertDesc, IsrEwDesc, IsrHeadDesc, IsrPoolDesc, IsrTailDesc, IsrView, IsrWgrad9Desc, IsrWgradDesc, TILE_H, TILE_W, check
 
 
+# Bumped whenever a libisr kernel writes parameters in place (FusedAdam.step,
+# ema_update_).  Raw-pointer writes do not bump torch's tensor `_version`, so the
+# packed-weight caches (models._Generator._packed, Denoise._packed) key on this too.
+_PARAM_EPOCH = [0]
+
+
+def param_write_epoch() -> int:
+    return _PARAM_EPOCH[0]
+
+
+def bump_param_epoch() -> None:
+    _PARAM_EPOCH[0] += 1
+
+
 def round_up(v: int, m: int) -> int:
     return (v + m - 1) // m * m
 

@@ -154,6 +154,7 @@ class FusedAdam(torch.optim.Optimizer):
                                      weight_decay=group["weight_decay"], bc2_sqrt=math.sqrt(1.0 - b2 ** t))
                 _lib.check(lib.isr_mt_adam(pt.data_ptr(), ch.data_ptr(), n, ctypes.byref(a),
                                            None, ops._stream()), "isr_mt_adam")
+                ops.bump_param_epoch()  # packed-weight caches must repack (raw-pointer writes)
         return loss
 
 
@@ -206,3 +207,4 @@ def ema_update_(ema: list[torch.Tensor], model: list[torch.Tensor], d: float) ->
         rows.append((v.data_ptr(), m.data_ptr(), 0, 0, v.numel()))
     pt, ch, n = _EMA_CACHE.get(rows, ema[0].device)
     _lib.check(_lib.load().isr_mt_lerp(pt.data_ptr(), ch.data_ptr(), n, float(d), ops._stream()), "isr_mt_lerp")
+    ops.bump_param_epoch()

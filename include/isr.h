@@ -305,8 +305,10 @@ int isr_pack_tail9x9(const float* w_oihw, void* packed, int32_t cout, int32_t ci
 int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s);
 /* Tuning entry point: same contract as isr_conv3x3_fwd with an explicit kernel
  * variant (0 = the production choice; others are tile / pipeline alternatives
- * kept for on-device A/B measurement).  Returns ISR_ERR_UNSUPPORTED for an
- * unknown variant. */
+ * kept for on-device A/B measurement).  Every variant of a default build writes
+ * the same outputs as variant 0 (up to fp32 summation order); timing-only
+ * ablations exist only in a library built with -DISR_TUNING.  Returns
+ * ISR_ERR_UNSUPPORTED for an unknown variant. */
 int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_t s);
 int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s);
 int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);

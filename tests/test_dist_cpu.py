@@ -25,7 +25,7 @@ def _worker(rank, world, port, q):
         with torch.enable_grad():
             m(x).pow(2).sum().backward()
         allreduce_grads(m.parameters())
-        q.put((rank, [p.grad.clone() for p in m.parameters()]))
+        q.put((rank, [p.grad.numpy().copy() for p in m.parameters()]))
     finally:
         dist.destroy_process_group()
 
@@ -37,7 +37,7 @@ def test_allreduce_grads_matches_full_batch_mean():
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(2))
+    res = {r: [torch.from_numpy(a) for a in v] for r, v in (q.get(timeout=120) for _ in range(2))}
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -57,7 +57,7 @@ def _mean_worker(rank, world, port, q):
     try:
         from image_super_resolution_amd.train_engine import allreduce_mean
         ts = [torch.full((3, 2), float(rank + 1)), torch.arange(4.0) * (rank + 1), torch.tensor([float(rank)])]
-        q.put((rank, [t.clone() for t in allreduce_mean(ts)]))
+        q.put((rank, [t.numpy().copy() for t in allreduce_mean(ts)]))
     finally:
         dist.destroy_process_group()
 
@@ -70,7 +70,7 @@ def test_allreduce_mean_flat_bucket():
     ps = [ctx.Process(target=_mean_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(2))
+    res = {r: [torch.from_numpy(a) for a in v] for r, v in (q.get(timeout=120) for _ in range(2))}
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -10,8 +10,10 @@ as the reference; checkpoints hold state_dicts (loaded with weights_only=True),
 see checkpoint.py.  Data: `--data` takes a directory of images or a JSON list
 (the reference reads ./train_images.json); without one, or with --synthetic,
 smooth random crops are generated on the GPU.  `--steps` caps iterations per
-epoch.  Generator training on the HIP path currently covers EResNet
-(`--enchant`); ResNet's train-mode BatchNorm is not implemented yet.
+epoch.  Every mode trains on the HIP path: ResNet (train-mode BatchNorm kernels)
+and EResNet (`--enchant`) in `--resnet` pixel-loss mode and in SRGAN mode (VGG
+perceptual + adversarial, discriminator on libisr), and the Denoise model
+(`--train_denoise`).
 """
 from __future__ import annotations
 
@@ -49,6 +51,7 @@ class _Batches:
             from torch.utils.data import DataLoader, DistributedSampler
             ds = data.SRCropDataset(opt.data, target, opt.scale, "Train: ")
             sampler = DistributedSampler(ds, world, rank, shuffle=True, seed=opt.seed) if world > 1 else None
+            self.sampler = sampler
             self.src = DataLoader(ds, batch_size=opt.batch_size, shuffle=sampler is None, sampler=sampler,
                                   num_workers=opt.worker, drop_last=True, pin_memory=True, persistent_workers=opt.worker > 0)
             self.n = len(self.src)
@@ -57,12 +60,23 @@ class _Batches:
         return self.n
 
     def __iter__(self):
+        """One endless iterator shared by every epoch (trainer.train takes `steps`
+        batches per epoch from it), so --steps below the loader length walks on
+        through the data instead of restarting at its head; each pass over the
+        loader reshuffles (DistributedSampler.set_epoch per pass, as shuffle=True
+        does for the reference's single-process loader)."""
         if self.synthetic:
             return self.src
-        def gen():
-            while True:
-                yield from self.src
-        return gen()
+        if getattr(self, "_it", None) is None:
+            def gen():
+                npass = 0
+                while True:
+                    if self.sampler is not None:
+                        self.sampler.set_epoch(npass)
+                    yield from self.src
+                    npass += 1
+            self._it = gen()
+        return self._it
 
 
 def main(opt):
@@ -100,7 +114,7 @@ def main(opt):
     if opt.train_denoise:  # train.py:204-243 of the reference
         dn_ck = work_dir / f"denoise_{opt.save_name}_{opt.rs_deep}_{opt.add_rate}.pt"
         model = models.Denoise(opt.rs_deep)
-        ema = models.ModelEMA(model, tau=opt.epochs * iters)
+        ema = models.ModelEMA(model)  # reference train.py:206: default tau (2000)
         model.to(device)
         ema.ema.to(device)
         optimizer = optim.FusedAdam(model.parameters(), lr=opt.lr)
