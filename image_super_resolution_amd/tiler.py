@@ -89,22 +89,50 @@ def shard_tiles(tiles: Sequence[Tile], world: int) -> list[list[Tile]]:
 BatchRunner = Callable[[torch.Tensor], torch.Tensor]  # uint8 [b,3,h,w] → uint8 [b,3,s·h,s·w]
 
 
-class GeneratorRunner:
-    """uint8 batch runner on the HIP generator: one plan (engine.make_plan) per (b, h, w)."""
+def plan_bytes(n: int, h: int, w: int, n_scalers: int) -> int:
+    """Device bytes of one generator plan's activation buffers (engine.GeneratorBuffers):
+    feat + 3 dense 192-ch buffers at LR, one 64-ch buffer per PixelShuffle stage."""
+    from .ops import TILE_H, TILE_W, round_up
+    ha, wa = round_up(h, TILE_H), round_up(w, TILE_W)
+    b = (64 + 3 * 192) * (ha + 2) * (wa + 2) * 2
+    for s in range(n_scalers):
+        ha, wa = 2 * ha, 2 * wa
+        p = 4 if s == n_scalers - 1 else 1
+        b += 64 * (ha + 2 * p) * (wa + 2 * p) * 2
+    return n * b
 
-    def __init__(self, gw: engine.GeneratorWeights, mean, std, device):
+
+class GeneratorRunner:
+    """uint8 batch runner on the HIP generator: one plan (engine.make_plan) per (b, h, w),
+    kept in a least-recently-used cache bounded by `max_plans` and `max_bytes` (plan
+    activation buffers; a 4 x 576² cfg4 plan is ~5 GB), so a still with many ragged
+    tile shapes does not hold one full set of buffers per shape."""
+
+    def __init__(self, gw: engine.GeneratorWeights, mean, std, device, max_plans: int = 16,
+                 max_bytes: int = 32 << 30):
+        from collections import OrderedDict
         self.gw, self.mean, self.std, self.device = gw, tuple(mean), tuple(std), torch.device(device)
         self.scale = 2 ** len(gw.scalers)
-        self.plans: dict[tuple[int, int, int], object] = {}
+        self.max_plans, self.max_bytes = max(1, max_plans), max_bytes
+        self.plans: "OrderedDict[tuple[int, int, int], object]" = OrderedDict()
+
+    def cached_bytes(self) -> int:
+        return sum(plan_bytes(n, h, w, len(self.gw.scalers)) for n, h, w in self.plans)
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if x.dtype != torch.uint8 or not x.is_cuda:
             raise ValueError("GeneratorRunner expects a uint8 CUDA batch")
         n, _, h, w = x.shape
-        plan = self.plans.get((n, h, w))
+        key = (n, h, w)
+        plan = self.plans.get(key)
         if plan is None:
+            need = plan_bytes(n, h, w, len(self.gw.scalers))
+            while self.plans and (len(self.plans) >= self.max_plans or self.cached_bytes() + need > self.max_bytes):
+                self.plans.popitem(last=False)  # evict least recently used (its buffers return to torch's pool)
             plan = engine.make_plan(self.gw, n, h, w, self.device, True, True, self.mean, self.std)
-            self.plans[(n, h, w)] = plan
+            self.plans[key] = plan
+        else:
+            self.plans.move_to_end(key)
         out = torch.empty(plan.out_shape, dtype=torch.uint8, device=self.device)
         return plan.run(x.contiguous(), out)
 

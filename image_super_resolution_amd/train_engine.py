@@ -392,8 +392,9 @@ class GeneratorTrainPlan:
             # data-parallel: one RCCL all-reduce of the whole flat gradient buffer
             # (47.5 MB for the 16-block generator) instead of DDP's per-bucket hooks
             import torch.distributed as dist
-            dist.all_reduce(grads, group=group if group is not True else None)
-            grads.div_(dist.get_world_size(group if group is not True else None))
+            g = group if group is not True else None
+            all_reduce_(grads, g)
+            grads.div_(dist.get_world_size(g))
         out = []
         for p, off in zip(self._params, self._goff):
             out.append(grads[off:off + p.numel()].view(p.shape))
@@ -448,6 +449,39 @@ def enable_grad_allreduce(gen: nn.Module, group=True) -> None:
     gen.__dict__["_isr_grad_group"] = group
 
 
+def all_reduce_(t: torch.Tensor, group=None) -> None:
+    """In-place SUM all-reduce: RCCL on device tensors; with the gloo backend (several
+    ranks rehearsing on one GPU, or CPU tests) device tensors are staged through host
+    memory, since gloo reduces host buffers."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group)
+
+
+def broadcast_params(params, src: int = 0, group=None) -> None:
+    """DDP's initial sync: every parameter from rank `src` as one flat broadcast."""
+    import torch.distributed as dist
+    ps = [p for p in params]
+    if not ps:
+        return
+    flat = torch.cat([p.detach().reshape(-1) for p in ps])
+    if flat.is_cuda and dist.get_backend(group) == "gloo":
+        h = flat.cpu()
+        dist.broadcast(h, src, group=group)
+        flat.copy_(h)
+    else:
+        dist.broadcast(flat, src, group=group)
+    off = 0
+    with torch.no_grad():
+        for p in ps:
+            p.copy_(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+
+
 def allreduce_mean(tensors: list, group=None) -> list:
     """Mean of `tensors` over the process group as ONE flat all-reduce (RCCL on the
     GPU, gloo in the CPU tests) — DDP's averaging with a single bucket.  Returns views
@@ -456,7 +490,7 @@ def allreduce_mean(tensors: list, group=None) -> list:
     if not tensors:
         return []
     flat = torch.cat([t.reshape(-1) for t in tensors])
-    dist.all_reduce(flat, group=group)
+    all_reduce_(flat, group)
     flat.div_(dist.get_world_size(group))
     out, off = [], 0
     for t in tensors:

@@ -209,6 +209,7 @@ def main():
     ups = np.array([1, 10, 100, 1000, 5000])
     np.savez_compressed(OUT / "ema.npz", updates=ups, decay=np.array([ema.decay(int(u)) for u in ups]), tau=2000)
     golden_denoise(M)
+    golden_disc(M)
     print("done")
 
 
@@ -226,13 +227,39 @@ def golden_denoise(M):
     print("denoise", tuple(y.shape))
 
 
+def golden_disc(M):
+    """11. Discriminator(3, 64, 8, 1024) (utils/models.py:513-569) in train mode, fp32,
+    as SRGAN training runs it (train.py:307, :113-126): logits for a [4,3,64,64]
+    input, then backward of sum(logits * w) — input gradient, every parameter
+    gradient (tensors above 16384 elements: their first 16384 flattened elements,
+    to keep the fixture small), and the BatchNorm running statistics after that
+    forward."""
+    torch.manual_seed(0)
+    model = load_synth(M.Discriminator(3, 64, 8, 1024), 40).train()
+    g = torch.Generator().manual_seed(41)
+    x = (torch.randn(4, 3, 64, 64, generator=g)).requires_grad_(True)
+    w = torch.randn(4, 1, generator=g)
+    with torch.enable_grad():
+        y = model(x)
+        (y * w).sum().backward()
+    out = dict(x=np32(x), w=np32(w), y=np32(y), dx=np32(x.grad), seed=40)
+    for k, p in model.named_parameters():
+        out[f"grad:{k}"] = np32(p.grad.flatten()[:16384])
+    for k, b in model.named_buffers():
+        if "running" in k:
+            out[f"stat:{k}"] = np32(b)
+    np.savez_compressed(OUT / "disc.npz", **out)
+    print("disc", tuple(y.shape), len(out))
+
+
 if __name__ == "__main__":
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
-    if sys.argv[1:2] == ["--only-denoise"]:  # regenerate just this fixture
+    only = {"--only-denoise": golden_denoise, "--only-disc": golden_disc}.get(sys.argv[1] if sys.argv[1:] else "")
+    if only is not None:  # regenerate just this fixture
         if not REF.exists():
             raise SystemExit("reference not present")
         install_stubs()
         import utils.models as _M  # reference
-        golden_denoise(_M)
+        only(_M)
     else:
         main()

@@ -154,3 +154,46 @@ def test_frozen_parameters_skip_weight_gradients():
     o.float().sum().backward()
     assert torch.equal(xr.grad, dx_full)
     assert all(p.grad is None for p in hip.parameters())
+
+
+def _disc_from_golden(g):
+    from image_super_resolution_amd.weights import synth_state_dict
+    m = models.Discriminator(3, 64, 8, 1024)
+    m.load_state_dict(synth_state_dict(m.state_dict(), int(g["seed"])))
+    return m.train()
+
+
+def _grads_vs(g, m, x, w, autocast=False):
+    o, dx, grads = _run(m, x, w, autocast)
+    names = [k for k, _ in m.named_parameters()]
+    return o, dx, {k: gr.flatten()[:16384] for k, gr in zip(names, grads)}
+
+
+def test_discriminator_vs_reference_golden(golden):
+    """pin D to the reference itself (tests/golden/disc.npz, the reference's
+    Discriminator(3,64,8,1024) in train mode, utils/models.py:513-569): logits, input
+    gradient, parameter gradients and BN running stats of the HIP discriminator vs the
+    reference's fp32 outputs.  Bar for gradients: the error torch's own bf16 autocast
+    makes against the same golden on the same tensors (the reference trains D under
+    fp16 autocast, train.py:91, :114): hip <= 1.3 x autocast + 0.02."""
+    from conftest import t
+    g = golden("disc")
+    x, w = t(g["x"]).to(DEV), t(g["w"]).to(DEV)
+    hip = _disc_from_golden(g).to(DEV).use_libisr(True)
+    amp = _disc_from_golden(g).to(DEV)
+    oh, dxh, gh = _grads_vs(g, hip, x, w)
+    oa, dxa, ga = _grads_vs(g, amp, x, w, autocast=True)
+    y_ref, dx_ref = t(g["y"]).to(DEV), t(g["dx"]).to(DEV)
+    assert _rel(oh, y_ref) < 0.03, _rel(oh, y_ref)
+    assert _rel(dxh, dx_ref) <= 1.3 * _rel(dxa, dx_ref) + 0.02, (_rel(dxh, dx_ref), _rel(dxa, dx_ref))
+    worst = []
+    for k in gh:
+        ref = t(g[f"grad:{k}"]).to(DEV)
+        eh, ea = _rel(gh[k], ref), _rel(ga[k], ref)
+        worst.append((eh, ea, k))
+        assert eh <= 1.3 * ea + 0.02, (k, eh, ea)
+    print("worst D grads (hip, autocast):", sorted(worst, reverse=True)[:3])
+    bufs = dict(hip.named_buffers())
+    for k in g:
+        if k.startswith("stat:"):
+            assert _rel(bufs[k[5:]], t(g[k]).to(DEV)) < 2e-2, k

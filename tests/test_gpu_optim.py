@@ -92,18 +92,21 @@ def test_ema_update_matches_reference_formula():
 def test_eval_repacks_after_hip_optimiser_and_ema_writes():
     """FusedAdam / ema_update_ write parameters through raw pointers (no
     torch `_version` bump); the packed-weight cache must still see the new weights."""
-    from image_super_resolution_amd.weights import synth_state_dict
+    from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_state_dict
     torch.manual_seed(0)
     m = models.EResNet(1, 0.2, scaleRate=2)
     m.load_state_dict(synth_state_dict(m.state_dict(), seed=3))
     m = m.to(DEV).eval()
-    x = torch.randn(1, 3, 16, 16, device=DEV)
+    lr, _ = synth_lr_batch(1, 16, 16, seed=8, scale=2)
+    x = normalize(lr).to(DEV)
     with torch.no_grad():
         y0 = m(x)
+    assert y0.abs().max().item() < 0.999  # not saturated: a weight change must show
     params = [p for p in m.parameters()]
-    opt = optim.FusedAdam(params, lr=1e-2)
+    opt = optim.FusedAdam(params, lr=1e-3)
+    g = torch.Generator(device=DEV).manual_seed(1)
     for p in params:
-        p.grad = torch.ones_like(p)
+        p.grad = torch.randn(p.shape, device=DEV, generator=g)
     opt.step()
     with torch.no_grad():
         y1 = m(x)
@@ -116,7 +119,7 @@ def test_eval_repacks_after_hip_optimiser_and_ema_writes():
     ema.__dict__.pop("_isr_pack", None)
     with torch.no_grad():
         ye0 = ema(x)
-        src = [p.detach().mul(0.5) for p in ema.parameters()]
+        src = [p.detach().mul(0.9) for p in ema.parameters()]
         optim.ema_update_([p.data for p in ema.parameters()], src, 0.5)
         ye1 = ema(x)
         fresh = copy.deepcopy(ema)

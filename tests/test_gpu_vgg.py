@@ -1,16 +1,18 @@
 """TruncatedVGG19 + gen_loss on the HIP path vs the reference's own outputs
 (tests/golden/loss_vgg_*.npz, produced by utils/loss.py with a seeded local
 VGG19 — ImageNet weights are unavailable offline, so parity with those is
-unpinned) and vs the fp32 oracle at a multi-tile size.
+unpinned) and vs the fp32 oracle at multi-tile sizes.
 
 bf16 activations through 16 convs: features and content loss are compared by
 relative L2 error (<= 3%).  The input gradient passes through 16 ReLU masks and
 4 maxpool argmaxes decided on bf16 activations; elements whose sign / window
-maximum flips between bf16 and fp32 reroute their gradient, so against fp32
-autograd only cos >= 0.9 holds (tools/diag_vgg.py: rel 2e-3 without
-ReLU/pool, growing with each switch; rounding differences between any two
-bf16 evaluations flip some of them too).  The backward kernels themselves are
-pinned exactly: a torch replay of the backward chain that takes every ReLU
+maximum flips between bf16 and fp32 reroute their gradient.  Its bar is
+therefore relative to the error torch's own bf16 autocast makes on the same
+tensors against the same fp32 reference (the reference trains under fp16
+autocast, train.py:91): rel(HIP) <= 1.3 x rel(autocast) + 0.02 — on white noise
+(the worst case for sign flips) and on a smooth 256² SR/HR pair from
+data.SyntheticSR (what SRGAN training feeds it).  The backward kernels themselves
+are pinned exactly: a torch replay of the backward chain that takes every ReLU
 mask and pool argmax from the HIP forward's own stored activations and rounds
 each gradient to bf16 as the HIP path stores it: rel <= 1%.
 """
@@ -59,9 +61,26 @@ def test_gen_loss_vs_reference_golden(golden, which):
     assert abs(adv.item() - float(g["adversarial"])) <= 1e-5
     gs = sr.grad.cpu()
     ref = t(g["grad_sr"])
-    assert F.cosine_similarity(gs.flatten(), ref.flatten(), dim=0).item() >= 0.9
+    sd = {k: v.float() for k, v in gl.vgg_net.state_dict().items()}
+    ga = _autocast_grad(sd, t(g["sr"]), t(g["hr"]), before_act=which == "preact")
+    eh, ea = _rel(gs, ref), _rel(ga, ref)
+    print(f"VGG input grad vs reference golden ({which}): HIP {eh:.4f}, torch bf16 autocast {ea:.4f}")
+    assert eh <= 1.3 * ea + 0.02, (eh, ea)
     d = gl.calc_advLoss(t(g["sr_disc"]).to(DEV), t(g["hr_disc"]).to(DEV))
     assert abs(d.item() - float(g["d_loss"])) <= 1e-5
+
+
+def _autocast_grad(sd, sr, hr, before_act):
+    """d content / d sr of the fp32 functional VGG (oracle graph) on the GPU under
+    torch's bf16 autocast: the rounding error torch's own mixed precision makes."""
+    sdd = {k: v.to(DEV) for k, v in sd.items()}
+    x = sr.to(DEV).clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        f = R.vgg_truncated(sdd, x, before_act=before_act)
+        fh = R.vgg_truncated(sdd, hr.to(DEV), before_act=before_act)
+    loss = F.l1_loss(f.float(), fh.float().detach()) if before_act else F.mse_loss(f.float(), fh.float().detach())
+    loss.backward()
+    return x.grad.float().cpu()
 
 
 def _replay_backward(vgg, plan, gfeat):
@@ -126,4 +145,39 @@ def test_vgg_multitile_vs_oracle():
     F.mse_loss(f, gl.vgg_net(hr.to(DEV)).detach()).backward()
     assert _rel(f.detach().cpu(), fr.detach()) < 3e-2
     gx, gr = x.grad.cpu(), srr.grad
-    assert F.cosine_similarity(gx.flatten(), gr.flatten(), dim=0).item() >= 0.9
+    ga = _autocast_grad(sd, sr, hr, before_act=False)
+    eh, ea = _rel(gx, gr), _rel(ga, gr)
+    print(f"VGG input grad vs fp32 oracle (noise 64x96): HIP {eh:.4f}, torch bf16 autocast {ea:.4f}")
+    assert eh <= 1.3 * ea + 0.02, (eh, ea)
+
+
+@pytest.mark.parametrize("before_act", [True, False])
+def test_vgg_grad_smooth_sr_hr_pair(before_act):
+    """SRGAN training's input: a smooth 256² HR crop and an SR close to it (HR plus
+    a smooth perturbation), ImageNet-normalised as train_srgan does; content loss
+    L1 on conv5_4 pre-ReLU (beforeAct, cfg3) / MSE post-ReLU; input gradient vs the
+    fp32 oracle with the autocast-relative bar."""
+    from image_super_resolution_amd import data
+    torch.set_num_threads(max(1, min(16, len(__import__("os").sched_getaffinity(0)))))
+    gl = _gl(before_act, 21)
+    src = data.SyntheticSR(2, 256, seed=4, device="cpu")
+    hr8, other8 = next(src), next(src)
+    mean = torch.tensor(data.IMAGENET_MEAN).view(1, 3, 1, 1)
+    std = torch.tensor(data.IMAGENET_STD).view(1, 3, 1, 1)
+    hr01, o01 = hr8.float() / 255, other8.float() / 255
+    sr01 = (0.85 * hr01 + 0.15 * o01).clamp(0, 1)
+    hr, sr = (hr01 - mean) / std, (sr01 - mean) / std
+    sd = {k: v.float().cpu() for k, v in gl.vgg_net.state_dict().items()}
+    srr = sr.clone().requires_grad_(True)
+    fr = R.vgg_truncated(sd, srr, before_act=before_act)
+    fhr = R.vgg_truncated(sd, hr, before_act=before_act)
+    (F.l1_loss(fr, fhr) if before_act else F.mse_loss(fr, fhr)).backward()
+    x = sr.to(DEV).requires_grad_(True)
+    f = gl.vgg_net(x)
+    fh = gl.vgg_net(hr.to(DEV)).detach()
+    (F.l1_loss(f, fh) if before_act else F.mse_loss(f, fh)).backward()
+    assert _rel(f.detach().cpu(), fr.detach()) < 3e-2
+    ga = _autocast_grad(sd, sr, hr, before_act)
+    eh, ea = _rel(x.grad.cpu(), srr.grad), _rel(ga, srr.grad)
+    print(f"VGG input grad, smooth 256² pair (beforeAct={before_act}): HIP {eh:.4f}, autocast {ea:.4f}")
+    assert eh <= 1.3 * ea + 0.02, (eh, ea)

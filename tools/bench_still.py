@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""cfg4 benchmark (BASELINE.json configs[3]): a 3840x2160 uint8 still → 15360x8640
+through the HIP tiler (rs.py image branch: 512-px windows, here with a 32-px halo),
+ResNet(16, 0.2, x4) with synthetic weights, tiles batched per shape.
+
+One process per GPU (torch.distributed.run for N > 1): tiles are dealt
+longest-processing-time-first over the ranks (tiler.shard_tiles, no data-path
+collective), rank 0 receives finished tiles point-to-point and owns the canvas.
+Reports HR megapixels/s of the whole image (after one warm-up call that builds
+the plans), seconds per image, and peak device memory.
+usage: python tools/bench_still.py [--reps 3] [--batch 4] [--halo 32]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from image_super_resolution_amd import models, tiler  # noqa: E402
+from image_super_resolution_amd.weights import synth_state_dict  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--window", type=int, default=512)
+    ap.add_argument("--halo", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--blocks", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    net = models.ResNet(args.blocks, 0.2, scaleRate=4)
+    net.load_state_dict(synth_state_dict(net.state_dict(), seed=4))
+    model = models.Model(net)
+    model.init_normalize([0.485, 0.456, 0.406], [0.229, 0.224, 0.225])
+    model = model.eval().fuse().to(dev)
+    g = torch.Generator().manual_seed(21)
+    lo = torch.rand(1, 3, args.height // 32, args.width // 32, generator=g)
+    img = torch.nn.functional.interpolate(lo, size=(args.height, args.width), mode="bicubic")
+    img = (img.clamp(0, 1)[0] * 255).round().to(torch.uint8)
+    runner = tiler.runner_for(model, dev)
+    up = tiler.TileUpscaler(runner, 4, window=args.window, halo=args.halo, batch=args.batch, device=dev)
+    torch.cuda.reset_peak_memory_stats(dev)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        up(img, rank=rank, world=world)  # warm-up: builds the plans
+        torch.cuda.synchronize()
+        warm = time.perf_counter() - t0
+        ts = []
+        for _ in range(args.reps):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            canvas = up(img, rank=rank, world=world)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            el = time.perf_counter() - t0
+            if world > 1:
+                tt = torch.tensor([el], device=dev, dtype=torch.float64)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                el = tt.item()
+            ts.append(el)
+    t = statistics.median(ts)
+    tiles = tiler.plan_tiles(args.height, args.width, args.window, args.halo)
+    run_px = sum(tt.cost for tt in tiles) * 16
+    res = {"metric": "cfg4 4K->16K still, HR MPix/s", "value": round(args.height * args.width * 16 / t / 1e6, 2),
+           "unit": "MPix/s", "n_gpus": world, "s_per_image": round(t, 4), "s_first_call": round(warm, 3),
+           "tiles": len(tiles), "window": args.window, "halo": args.halo, "batch": args.batch,
+           "shapes": sorted({tt.in_shape for tt in tiles}),
+           "halo_overhead": round(run_px / (args.height * args.width * 16), 4),
+           "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
+           "plans_cached": len(runner.plans), "plan_cache_gib": round(runner.cached_bytes() / 2**30, 2),
+           "canvas": list(canvas.shape) if canvas is not None else None}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+        if args.out:
+            Path(args.out).write_text(json.dumps(res, indent=1))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

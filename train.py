@@ -28,7 +28,7 @@ import torch
 from torch import nn
 
 from image_super_resolution_amd import checkpoint, data, loss as L, models, optim, trainer
-from image_super_resolution_amd.train_engine import enable_grad_allreduce
+from image_super_resolution_amd.train_engine import broadcast_params, enable_grad_allreduce
 
 
 def first_setup(seed):
@@ -79,6 +79,78 @@ class _Batches:
         return self._it
 
 
+def setup_resnet(opt, device, group, iters: int, res_ck: Path):
+    """`--resnet` pixel-loss mode (train.py:258-302 of the reference): generator,
+    EMA, loss, Adam and LinearLR, resumed from `res_ck` with --resume; with a process
+    group the gradient all-reduce is enabled and parameters broadcast from rank 0."""
+    model = (models.EResNet(opt.rs_deep, opt.add_rate, opt.scale) if opt.enchant
+             else models.ResNet(opt.rs_deep, opt.add_rate, scaleRate=opt.scale))
+    ema = models.ModelEMA(model, tau=opt.epochs * iters)
+    model.to(device)
+    ema.ema.to(device)
+    compute_loss = L.L1Loss().to(device) if opt.enchant else nn.MSELoss()
+    optimizer = optim.FusedAdam(model.parameters(), lr=opt.lr, betas=(0.9, 0.999), weight_decay=opt.weight_decay)
+    schedule = torch.optim.lr_scheduler.LinearLR(optimizer, 1, opt.lr2, total_iters=opt.epochs * iters)
+    start = 0
+    if opt.resume and res_ck.is_file():
+        ck = checkpoint.load_checkpoint(res_ck)
+        sd = checkpoint.intersect_dicts({k: v.float() for k, v in ck["ema"].items()}, model.state_dict())
+        ema.ema.load_state_dict({k: v.float() for k, v in ck["ema"].items()})
+        ema.updates = ck["updates"]
+        model.load_state_dict(sd, strict=False)
+        if len(sd) == len(model.state_dict()):
+            if ck.get("optimizer") is not None:
+                optimizer.load_state_dict(ck["optimizer"])
+            start = ck["epoch"] + 1
+    if group is not None:
+        enable_grad_allreduce(model, group)
+        for p in model.parameters():  # identical start on every rank
+            torch.distributed.broadcast(p.data, 0)
+    return model, ema, compute_loss, optimizer, schedule, start
+
+
+def setup_srgan(opt, device, group, iters: int, gen_ck: Path, res_ck: Path):
+    """SRGAN-mode models, optimisers, schedules and loss (train.py:304-366 of the
+    reference), resumed from `gen_ck` with --resume; with a process group
+    (`group` not None) the generator's gradient all-reduce is enabled and every
+    parameter is broadcast from rank 0 (DDP's initial sync)."""
+    gen_net = models.SRGAN(opt.rs_deep, opt.add_rate, opt.enchant, opt.scale)
+    gen_net.init_weight(pretrained=res_ck.as_posix())
+    dis_net = models.Discriminator(3, 64, 8, 1024).use_libisr(not opt.dis_miopen)
+    ema = models.ModelEMA(gen_net, tau=opt.epochs * iters)
+    optimizer_g = optim.FusedAdam(gen_net.parameters(), lr=opt.lr, betas=(0.9, 0.999),
+                                   weight_decay=opt.weight_decay)
+    optimizer_d = optim.FusedAdam(dis_net.parameters(), lr=opt.lr, betas=(0.9, 0.999),
+                                   weight_decay=opt.weight_decay)
+    schedule_g = torch.optim.lr_scheduler.LinearLR(optimizer_g, 1, opt.lr2, total_iters=opt.epochs * iters)
+    schedule_d = torch.optim.lr_scheduler.LinearLR(optimizer_d, 1, opt.lr2, total_iters=opt.epochs * iters)
+    start = 0
+    if opt.resume and gen_ck.is_file():
+        ck = checkpoint.load_checkpoint(gen_ck)
+        gen_net.load_state_dict(checkpoint.intersect_dicts({k: v.float() for k, v in ck["ema"].items()},
+                                                           gen_net.state_dict()), strict=False)
+        dis_net.load_state_dict(checkpoint.intersect_dicts({k: v.float() for k, v in ck["dis_net"].items()},
+                                                           dis_net.state_dict()), strict=False)
+        if ck.get("optimizer_g") is not None:
+            optimizer_g.load_state_dict(ck["optimizer_g"])
+            optimizer_d.load_state_dict(ck["optimizer_d"])
+        ema.ema.load_state_dict({k: v.float() for k, v in ck["ema"].items()})
+        ema.updates = ck["updates"]
+        start = ck["epoch"] + 1
+    compute_loss = L.gen_loss(device=device, beforeAct=opt.enchant, vgg_weights=opt.vgg_weights)
+    gen_net.to(device)
+    if opt.dis_miopen:  # stock convs: NHWC (channels_last) + find mode, ~17 % faster than NCHW
+        dis_net.to(device, memory_format=torch.channels_last)
+        torch.backends.cudnn.benchmark = True
+    else:
+        dis_net.to(device)
+    ema.ema.to(device)
+    if group is not None:
+        enable_grad_allreduce(gen_net, group)
+        broadcast_params(list(gen_net.parameters()) + list(dis_net.parameters()))
+    return gen_net, dis_net, ema, optimizer_g, optimizer_d, schedule_g, schedule_d, compute_loss, start
+
+
 def main(opt):
     first_setup(opt.seed)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,7 +163,10 @@ def main(opt):
     group = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if opt.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)  # RCCL over xGMI
+        else:  # gloo: rehearsal of several ranks on one GPU (RCCL needs one GPU per rank)
+            dist.init_process_group(opt.dist_backend)
         group = True
     work_dir = Path(opt.work_dir)
     work_dir.mkdir(exist_ok=True)
@@ -131,8 +206,7 @@ def main(opt):
             print(f"Loaded pre-trained {len(sd)}/{len(model.state_dict())} model")
         if group is not None:
             enable_grad_allreduce(model, group)
-            for p in model.parameters():
-                torch.distributed.broadcast(p.data, 0)
+            broadcast_params(model.parameters())
         schedule = torch.optim.lr_scheduler.LinearLR(optimizer, 1, opt.lr2, total_iters=opt.epochs * iters)
         n_p = sum(p.numel() for p in model.parameters())
         print(f"Model: {n_p:,} parameters, {n_p:,} gradients")
@@ -147,29 +221,7 @@ def main(opt):
         return
 
     if opt.resnet:
-        model = (models.EResNet(opt.rs_deep, opt.add_rate, opt.scale) if opt.enchant
-                 else models.ResNet(opt.rs_deep, opt.add_rate, scaleRate=opt.scale))
-        ema = models.ModelEMA(model, tau=opt.epochs * iters)
-        model.to(device)
-        ema.ema.to(device)
-        compute_loss = L.L1Loss().to(device) if opt.enchant else nn.MSELoss()
-        optimizer = optim.FusedAdam(model.parameters(), lr=opt.lr, betas=(0.9, 0.999), weight_decay=opt.weight_decay)
-        schedule = torch.optim.lr_scheduler.LinearLR(optimizer, 1, opt.lr2, total_iters=opt.epochs * iters)
-        start = 0
-        if opt.resume and res_ck.is_file():
-            ck = checkpoint.load_checkpoint(res_ck)
-            sd = checkpoint.intersect_dicts({k: v.float() for k, v in ck["ema"].items()}, model.state_dict())
-            ema.ema.load_state_dict({k: v.float() for k, v in ck["ema"].items()})
-            ema.updates = ck["updates"]
-            model.load_state_dict(sd, strict=False)
-            if len(sd) == len(model.state_dict()):
-                if ck.get("optimizer") is not None:
-                    optimizer.load_state_dict(ck["optimizer"])
-                start = ck["epoch"] + 1
-        if group is not None:
-            enable_grad_allreduce(model, group)
-            for p in model.parameters():  # identical start on every rank
-                torch.distributed.broadcast(p.data, 0)
+        model, ema, compute_loss, optimizer, schedule, start = setup_resnet(opt, device, group, iters, res_ck)
         print(f"Train: ResNet {opt.epochs} epochs, {sum(p.numel() for p in model.parameters()):,} parameters")
         transform = data.GPUTransform(opt.scale, hr_norm=False, mean=mean, std=std, device=device)
         for epoch in range(start, opt.epochs):
@@ -182,41 +234,8 @@ def main(opt):
                                            loss=losses, scaler=scaler_gen.state_dict(), ema=ema.ema,
                                            updates=ema.updates)
     else:
-        gen_net = models.SRGAN(opt.rs_deep, opt.add_rate, opt.enchant, opt.scale)
-        gen_net.init_weight(pretrained=res_ck.as_posix())
-        dis_net = models.Discriminator(3, 64, 8, 1024).use_libisr(not opt.dis_miopen)
-        ema = models.ModelEMA(gen_net, tau=opt.epochs * iters)
-        optimizer_g = optim.FusedAdam(gen_net.parameters(), lr=opt.lr, betas=(0.9, 0.999),
-                                       weight_decay=opt.weight_decay)
-        optimizer_d = optim.FusedAdam(dis_net.parameters(), lr=opt.lr, betas=(0.9, 0.999),
-                                       weight_decay=opt.weight_decay)
-        schedule_g = torch.optim.lr_scheduler.LinearLR(optimizer_g, 1, opt.lr2, total_iters=opt.epochs * iters)
-        schedule_d = torch.optim.lr_scheduler.LinearLR(optimizer_d, 1, opt.lr2, total_iters=opt.epochs * iters)
-        start = 0
-        if opt.resume and gen_ck.is_file():
-            ck = checkpoint.load_checkpoint(gen_ck)
-            gen_net.load_state_dict(checkpoint.intersect_dicts({k: v.float() for k, v in ck["ema"].items()},
-                                                               gen_net.state_dict()), strict=False)
-            dis_net.load_state_dict(checkpoint.intersect_dicts({k: v.float() for k, v in ck["dis_net"].items()},
-                                                               dis_net.state_dict()), strict=False)
-            if ck.get("optimizer_g") is not None:
-                optimizer_g.load_state_dict(ck["optimizer_g"])
-                optimizer_d.load_state_dict(ck["optimizer_d"])
-            ema.ema.load_state_dict({k: v.float() for k, v in ck["ema"].items()})
-            ema.updates = ck["updates"]
-            start = ck["epoch"] + 1
-        compute_loss = L.gen_loss(device=device, beforeAct=opt.enchant, vgg_weights=opt.vgg_weights)
-        gen_net.to(device)
-        if opt.dis_miopen:  # stock convs: NHWC (channels_last) + find mode, ~17 % faster than NCHW
-            dis_net.to(device, memory_format=torch.channels_last)
-            torch.backends.cudnn.benchmark = True
-        else:
-            dis_net.to(device)
-        ema.ema.to(device)
-        if group is not None:
-            enable_grad_allreduce(gen_net, group)
-            for p in list(gen_net.parameters()) + list(dis_net.parameters()):
-                torch.distributed.broadcast(p.data, 0)
+        gen_net, dis_net, ema, optimizer_g, optimizer_d, schedule_g, schedule_d, compute_loss, start = \
+            setup_srgan(opt, device, group, iters, gen_ck, res_ck)
         print(f"Train: {opt.epochs} epochs, gen {sum(p.numel() for p in gen_net.parameters()):,} parameters, "
               f"dis {sum(p.numel() for p in dis_net.parameters()):,} parameters")
         transform = data.GPUTransform(opt.scale, hr_norm=True, mean=mean, std=std, device=device)
@@ -267,6 +286,8 @@ def parse(argv=None):
     p.add_argument("--data", type=str, default="", help="image directory or JSON list (default: ./train_images.json "
                    "if present, else synthetic)")
     p.add_argument("--synthetic", action="store_true")
+    p.add_argument("--dist_backend", default="nccl", help="process-group backend for WORLD_SIZE > 1 "
+                   "(nccl = RCCL; gloo only to rehearse several ranks sharing one GPU)")
     p.add_argument("--steps", type=int, default=0, help="iterations per epoch (0 = one pass over the data)")
     p.add_argument("--vgg_weights", type=str, default=None)
     p.add_argument("--dis_miopen", action="store_true", help="run the discriminator's conv stack on stock MIOpen "
