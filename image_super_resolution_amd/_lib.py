@@ -32,6 +32,11 @@ class IsrConvDesc(ctypes.Structure):
                 ("taps", c_int32)]
 
 
+class IsrChainDesc(ctypes.Structure):
+    _fields_ = [("layers", c_void_p), ("kinds", c_void_p), ("nl", c_int32), ("n", c_int32), ("ha", c_int32),
+                ("wa", c_int32), ("state", c_void_p), ("acquire", c_int32)]
+
+
 class IsrHeadDesc(ctypes.Structure):
     _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
                 ("cout", c_int32), ("x", c_void_p), ("x_u8", c_int32),
@@ -124,6 +129,10 @@ SIGNATURES = {
     "isr_pack_tail9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "isr_conv3x3_fwd": (c_int32, [POINTER(IsrConvDesc), c_void_p]),
     "isr_conv3x3_fwd_variant": (c_int32, [POINTER(IsrConvDesc), c_int32, c_void_p]),
+    "isr_tuning_conv_stamps": (c_int32, [c_void_p]),
+    "isr_conv3x3_check": (c_int32, [POINTER(IsrConvDesc)]),
+    "isr_conv_chain_state_words": (c_size_t, [c_int32, c_int32, c_int32]),
+    "isr_conv_chain": (c_int32, [POINTER(IsrChainDesc), c_void_p]),
     "isr_head9x9_fwd": (c_int32, [POINTER(IsrHeadDesc), c_void_p]),
     "isr_tail9x9_fwd": (c_int32, [POINTER(IsrTailDesc), c_void_p]),
     "isr_tail9x9_fwd_variant": (c_int32, [POINTER(IsrTailDesc), c_int32, c_void_p]),

@@ -10,6 +10,9 @@
 namespace isr {
 int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s);
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s);
+int conv_stamps_set(void* p);
+size_t conv_chain_state_words(int n, int ha, int wa);
+int conv_chain(const isr_chain_desc* c, hipStream_t s);
 size_t conv3x3_packed_bytes(int cout, int cin);
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s);
@@ -211,6 +214,27 @@ int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s) {
     int rc = conv3x3_validate(d);
     if (rc != ISR_OK) return rc;
     return launched(isr::conv3x3_fwd_dispatch(d, (hipStream_t)s), "conv3x3");
+}
+
+int isr_conv3x3_check(const isr_conv_desc* d) { return conv3x3_validate(d); }
+
+size_t isr_conv_chain_state_words(int32_t n, int32_t ha, int32_t wa) {
+    if (n <= 0 || ha <= 0 || wa <= 0 || ha % 16 || wa % 32) return 0;
+    return isr::conv_chain_state_words(n, ha, wa);
+}
+
+int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s) {
+    if (!c || !c->layers || !c->kinds || !c->state || c->nl <= 0)
+        return fail(ISR_ERR_BAD_DESC, "conv chain: null layers / kinds / state or nl <= 0");
+    if (c->n <= 0 || c->ha <= 0 || c->wa <= 0 || c->ha % 16 || c->wa % 32)
+        return fail(ISR_ERR_BAD_DESC, "conv chain: bad grid n=%d ha=%d wa=%d", c->n, c->ha, c->wa);
+    return launched(isr::conv_chain(c, (hipStream_t)s), "conv chain");
+}
+
+int isr_tuning_conv_stamps(void* buf) {
+    const int rc = isr::conv_stamps_set(buf);
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "conv stamps: library built without -DISR_TUNING");
+    return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "conv stamps: hipMemcpyToSymbol failed");
 }
 
 int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_t s) {

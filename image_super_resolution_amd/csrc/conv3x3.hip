@@ -24,13 +24,46 @@
 
 namespace isr {
 
+// Timing stamps (tuning builds only, isr_tuning_conv_stamps): per block, wall-clock
+// (s_memrealtime, 100 MHz) at entry / first chunk landed / main loop done / epilogue
+// done, plus the raw HW_ID and XCC_ID registers.  Written by a vector store of lane 0
+// of wave 0 into a buffer of its own (never read by the kernel).
+#ifdef ISR_TUNING
+__device__ unsigned long long* g_conv_stamps;
+#endif
+__device__ __forceinline__ void conv_stamp(int slot, int row = -1) {
+#ifdef ISR_TUNING
+    unsigned long long* p = g_conv_stamps;
+    if (p != nullptr && threadIdx.x == 0 && row != -2) {
+        unsigned long long t;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");  // not hoistable
+        p[(size_t)(row < 0 ? blockIdx.x : row) * 8 + slot + threadIdx.x] = t;
+        if (slot == 0 && row < 0) {
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20); // HW_REG_XCC_ID
+            p[(size_t)blockIdx.x * 8 + 6 + threadIdx.x] = hw;
+            p[(size_t)blockIdx.x * 8 + 7 + threadIdx.x] = xcc;
+        }
+    }
+#else
+    (void)slot;
+    (void)row;
+#endif
+}
+
 template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1), int EPQ_ = 4,
-          int SPL_ = 1, int TWN_ = 0>
+          int SPL_ = 0, int TWN_ = 0>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
-    static constexpr int PIPE = PIPE_; // 1: double-buffered fragment registers across (k-step, dx) steps
+    // 1: double-buffered fragment registers across (k-step, dx) steps; 2: the next step's reads
+    // spread over the current step's MFMAs (front-loading them instead: 0.43-0.92x, register
+    // pressure)
+    static constexpr int PIPE = PIPE_;
     static constexpr int EPQ = EPQ_;   // epilogue operand units (8 VGPRs each) loaded per pass
-    static constexpr int SPL = SPL_;   // the next chunk's LDS-DMA issued in SPL parts, one before each of the first SPL steps
+    // refill placement: 0 = the next chunk's LDS-DMA issued right after the current chunk's
+    // step-0 fragment reads (PIPE 2; otherwise as 1), 1 = issued before them (round-1 order),
+    // > 1 = issued in SPL parts, one before each of the first SPL steps
+    static constexpr int SPL = SPL_;
     // tap window: 0 = all 3x3 taps; 1 = taps {0,1}^2; 2 = taps {1,2}^2 (the 2x2 convs that a
     // stride-2 3x3 conv and its transpose become on the 2x2 phase decomposition, isr_conv_desc.taps)
     static constexpr int TWN = TWN_;
@@ -38,11 +71,8 @@ struct C3 {
     static constexpr int TN = TWN ? 2 : 3;
     static constexpr int NA = R + TN - 1;  // input rows one wave reads per step
     static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol)
-    // Ablation bits, timing-only builds (outputs wrong): 1 = no MFMA (operands
+    // Ablation bits, tuning builds only (outputs wrong): 1 = no MFMA (operands
     // kept live), 2 = stage only chunk 0 (no refill), 4 = no epilogue stores.
-    // Experiment bits (outputs exact): 8/16 = blocks of the second dispatch round
-    // (blockIdx / 256 odd: the second block slot of each CU) start ~0.5/1 us late,
-    // so two co-resident blocks are out of phase (one's loads beside the other's MFMAs).
     static constexpr int ABL = ABL_;
     static constexpr int TH = R * WM;
     static constexpr int TW = 32;
@@ -87,8 +117,8 @@ __device__ __forceinline__ void swap_halves(float& lo, float& hi) {
 // MODE bits (compile-time: no per-element branches): 1 = r1, 2 = r2, 4 = y2, 8 = shuffle,
 // 16 = LeakyReLU' mask (backward).  r1_cn / m_c0 are multiples of 32, so their
 // channel tests are uniform per 32-cout fragment (scalar branches).
-template <class C, int MODE>
-__device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C::R][C::NF], int img, int ct,
+template <class C, int MODE, int HX, class Desc>
+__device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::NF], int img, int ct,
                                          int x0, int y0, int wave, int lane) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int R = C::R, NF = C::NF, CT = C::CT, EPS = C::EPS;
@@ -124,7 +154,7 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
                 }
                 if constexpr (MODE & 16) {  // LeakyReLU' of the (shuffled-grid) mask source, all channels
                     const bf16x8 mq =
-                        *reinterpret_cast<const bf16x8*>(view_at(d.m, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8));
+                        load16_hx<HX>(d.m, view_at(d.m, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8));
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
                         if (!((float)mq[k] > 0.f)) v[k] *= d.mslope;
@@ -133,7 +163,7 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
 #pragma unroll
                     for (int k = 0; k < 8; ++k) v[k] = 0.f;
                 }
-                store8_bf16(view_at(d.y, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8), v);
+                store8_bf16_hx<HX>(d.y, view_at(d.y, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8), v);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
@@ -161,11 +191,11 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
             for (int blk = 0; blk < 2; ++blk) {
                 const int co = cf + 16 * blk + 8 * hh;
                 if constexpr (MODE & 1) {
-                    if (use_r1) q1[buf][blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r1, img, yy, xx, co));
+                    if (use_r1) q1[buf][blk] = load16_hx<HX>(d.r1, view_at(d.r1, img, yy, xx, co));
                 }
-                if constexpr (MODE & 2) q2[buf][blk] = *reinterpret_cast<const bf16x8*>(view_at(d.r2, img, yy, xx, co));
+                if constexpr (MODE & 2) q2[buf][blk] = load16_hx<HX>(d.r2, view_at(d.r2, img, yy, xx, co));
                 if constexpr (MODE & 16) {
-                    if (use_m) qm[buf][blk] = *reinterpret_cast<const bf16x8*>(view_at(d.m, img, yy, xx, co));
+                    if (use_m) qm[buf][blk] = load16_hx<HX>(d.m, view_at(d.m, img, yy, xx, co));
                 }
             }
         };
@@ -211,8 +241,8 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
                     if (!valid) u[e] = 0.f;
                 }
                 const int co = cf + 16 * blk + 8 * hh;
-                store8_bf16(view_at(d.y, img, yy, xx, co), u);
-                if constexpr (MODE & 4) store8_bf16(view_at(d.y2, img, yy, xx, co), u);
+                store8_bf16_hx<HX>(d.y, view_at(d.y, img, yy, xx, co), u);
+                if constexpr (MODE & 4) store8_bf16_hx<HX>(d.y2, view_at(d.y2, img, yy, xx, co), u);
             }
         }
     }
@@ -220,14 +250,19 @@ __device__ __forceinline__ void epilogue(const isr_conv_desc& d, f32x16 (&acc)[C
 
 // Packed weights (isr_pack_conv3x3): [c16 = cin/16][tap 9][cout][hpos 2][8 bf16],
 // element = W[n][c16*16 + h*8 + e][tap], h = hpos ^ ((n >> 3) & 1).
-template <class C>
-__global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_desc d) {
+// XS2: the input is read as PixelShuffle(2)ᵀ (isr_conv_desc.x_sub2) — a template flag so the
+// common path carries no per-chunk address division.
+// One output tile (logical tile index t: cout tile innermost, then x, y, image) of the conv
+// described by `d`, computed by the whole workgroup.  HX = 1 (the persistent chain kernel,
+// conv_chain.hip): activations written by other workgroups of the same launch are read with
+// sc1 loads (L1 bypass) and the outputs stored write-through (sc1), Guideline 16's hand-off.
+template <class C, bool XS2, int HX, class Desc>
+__device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int R = C::R, NF = C::NF, WM = C::WM;
 
     const int nct = d.cout / C::CT;
     const int nbx = d.wa / C::TW, nby = d.ha / C::TH;
-    int t = xcd_remap(blockIdx.x, gridDim.x);
     const int ct = t % nct; t /= nct;
     const int bx = t % nbx; t /= nbx;
     const int by = t % nby;
@@ -239,30 +274,28 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     const int l31 = lane & 31;
     const int hh = lane >> 5;
     const int nchunks = C::CIN ? C::CIN / C::KC : d.cin / C::KC;
-    if constexpr (C::ABL & 24) {
-        if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_sleep((C::ABL & 8) ? 16 : 32);
-    }
+    conv_stamp(0, srow);
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
     // x_sub2 (backward of PixelShuffle): halo pixel (row, col) of sub-position s
     // lives at x pixel (2row + (s>>1), 2col + (s&1)) — pixel stride 2 plus a
     // per-chunk offset.
-    const int ps = d.x_sub2 ? 2 : 1;
+    const int ps = XS2 ? 2 : 1;
     const char* xbase = view_at(d.x, img, ps * (y0 - 1), ps * (x0 - 1), 0);
     const size_t pstride = plane_bytes(d.x);
     const char* wbase = (const char*)d.wpack;
     const int xrow_bytes = d.x.wp * 32;
     auto xchunk = [&](int chunk) -> size_t {
-        if (!d.x_sub2) return (size_t)chunk * C::KS * pstride;
+        if constexpr (!XS2) return (size_t)chunk * C::KS * pstride;
         const int cs4 = d.cin >> 2;
         const int c0 = chunk * C::KC;
         const int sp = c0 / cs4, cb = (c0 - sp * cs4) >> 4;
         return (size_t)cb * pstride + (size_t)(sp >> 1) * xrow_bytes + (sp & 1) * 32;
     };
     const size_t wchunk_bytes = (size_t)C::KS * 9 * d.cout * 32;
-    uint32_t off[C::IPW];
-#pragma unroll
-    for (int k = 0; k < C::IPW; ++k) {
+    // recomputed per stage instead of held in IPW registers (the wide kernel sits at the
+    // 256-VGPR limit of two waves per SIMD)
+    auto off_of = [&](int k) -> uint32_t {
         const int j = wave + WM * k;
         uint32_t o = 0;
         if (j < C::HALO_INSTR) {
@@ -281,8 +314,8 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
             const int rem = u - seg * (C::CT * 2);
             o = (uint32_t)((seg * d.cout + ct * C::CT) * 32 + rem * 16);
         }
-        off[k] = o;
-    }
+        return o;
+    };
 
     auto stage = [&](int chunk, int buf, int k0 = 0, int k1 = C::IPW) {
         char* dst = smem + buf * C::STAGE;
@@ -291,8 +324,13 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
 #pragma unroll
         for (int k = k0; k < k1; ++k) {
             const int j = wave + WM * k;
-            const char* src = (j < C::HALO_INSTR ? xs : ws) + off[k];
-            glds16(src, dst + j * 1024);
+            const uint32_t o = off_of(k);
+            if (j < C::HALO_INSTR) {
+                if constexpr (HX) glds16_sc1(xs + o, dst + j * 1024);
+                else glds16(xs + o, dst + j * 1024);
+            } else {
+                glds16(ws + o, dst + j * 1024);
+            }
         }
     };
 
@@ -327,8 +365,9 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        if (chunk == 0) conv_stamp(1, srow);
         const bool refill = !(C::ABL & 2) && chunk + C::NST - 1 < nchunks;
-        if constexpr (C::SPL <= 1) {
+        if constexpr (C::SPL == 1 || (C::SPL == 0 && C::PIPE != 2)) {
             if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
         }
 
@@ -353,18 +392,6 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
                 }
 #pragma unroll
             for (int ia = 0; ia < NA; ++ia) {
-                if constexpr (C::ABL & 32) {
-                    // timing probe: dx > TLO fragments = previous dx's shifted one lane by DPP
-                    // (lanes 31/63 not fixed up: outputs wrong)
-                    if (st % TN != 0) {
-                        const int prev = C::PIPE ? set ^ 1 : set;
-                        auto* src = reinterpret_cast<int*>(&fa[prev][ia]);
-                        auto* dst = reinterpret_cast<int*>(&fa[set][ia]);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) dst[e] = __builtin_amdgcn_update_dpp(0, src[e], 0x130, 0xf, 0xf, false);
-                        continue;
-                    }
-                }
                 const int q = qw + (TLO + ia) * C::HC + dx;
                 fa[set][ia] = lds_read16(hp + halo_unit2(q, hh) * 16);
             }
@@ -384,7 +411,15 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
             }
         };
         if constexpr (C::PIPE) load_step(0, 0);
-        if constexpr (C::PIPE == 2) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (C::PIPE == 2) {
+            // the refill's LDS-DMA issue (10-16 instructions, scalar address math) runs while
+            // step 0's fragment reads are in flight, instead of ahead of them
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (C::SPL == 0) {
+                if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int st = 0; st < NS; ++st) {
             const int cur = C::PIPE ? (st & 1) : 0;
@@ -401,6 +436,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
                 constexpr int NRD = TN * NF + NA;  // reads per step
                 constexpr int NM = R * TN * NF;    // MFMAs per step
                 int m = 0;
+
 #pragma unroll
                 for (int ia = 0; ia < NA; ++ia)
 #pragma unroll
@@ -437,16 +473,6 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
                         for (int f = 0; f < NF; ++f) {
                             if constexpr (C::ABL & 1) {
                                 asm volatile("" ::"v"(fa[cur][ia]), "v"(fb[cur][dyi][f]));
-                            } else if constexpr (C::ABL & 64) {
-                                // DVFS probe (outputs wrong): the same FLOPs as two 16x16x32 MFMAs
-                                f32x16& a = acc[r][f];
-                                const int h = (r + f) & 1;
-                                f32x4 c0 = {a[8 * h], a[8 * h + 1], a[8 * h + 2], a[8 * h + 3]};
-                                f32x4 c1 = {a[8 * h + 4], a[8 * h + 5], a[8 * h + 6], a[8 * h + 7]};
-                                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][dyi][f], fa[cur][ia], c0, 0, 0, 0);
-                                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[cur][dyi][f], fa[cur][ia], c1, 0, 0, 0);
-#pragma unroll
-                                for (int e = 0; e < 4; ++e) { a[8 * h + e] = c0[e]; a[8 * h + 4 + e] = c1[e]; }
                             } else {
                                 acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
                             }
@@ -458,6 +484,7 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier(); // all waves done reading the ring before it becomes the epilogue image
+    conv_stamp(2, srow);
 
     if constexpr (C::ABL & 4) {
         if (d.n < 0) { // never true: keeps the accumulators (and so the MFMAs) live
@@ -475,33 +502,60 @@ __global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_des
     // ---- epilogue (mode picked once, wave-uniform, so no per-element branches)
     const int mode = d.shuffle == 2 ? (d.m.data ? 24 : 8)
                                     : ((d.r1.data ? 1 : 0) | (d.r2.data ? 2 : 0) | (d.y2.data ? 4 : 0) | (d.m.data ? 16 : 0));
-    switch (mode) {
-        case 0: epilogue<C, 0>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 1: epilogue<C, 1>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 2: epilogue<C, 2>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 3: epilogue<C, 3>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 4: epilogue<C, 4>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 5: epilogue<C, 5>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 6: epilogue<C, 6>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 7: epilogue<C, 7>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 8: epilogue<C, 8>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 24: epilogue<C, 24>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 16: epilogue<C, 16>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 17: epilogue<C, 17>(d, acc, img, ct, x0, y0, wave, lane); break;
-        case 18: epilogue<C, 18>(d, acc, img, ct, x0, y0, wave, lane); break;
-        default: epilogue<C, 19>(d, acc, img, ct, x0, y0, wave, lane); break;  // 19; y2 + mask is rejected by isr_conv3x3_fwd
+    if constexpr (HX) {  // chain layers: growth (plain store) or the RDB final conv (r1 [+ r2])
+        if (mode == 0) epilogue<C, 0, HX>(d, acc, img, ct, x0, y0, wave, lane);
+        else if (mode == 1) epilogue<C, 1, HX>(d, acc, img, ct, x0, y0, wave, lane);
+        else epilogue<C, 3, HX>(d, acc, img, ct, x0, y0, wave, lane);
+    } else switch (mode) {
+        case 0: epilogue<C, 0, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 1: epilogue<C, 1, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 2: epilogue<C, 2, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 3: epilogue<C, 3, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 4: epilogue<C, 4, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 5: epilogue<C, 5, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 6: epilogue<C, 6, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 7: epilogue<C, 7, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 8: epilogue<C, 8, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 24: epilogue<C, 24, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 16: epilogue<C, 16, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 17: epilogue<C, 17, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 18: epilogue<C, 18, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        default: epilogue<C, 19, HX>(d, acc, img, ct, x0, y0, wave, lane); break;  // 19; y2 + mask is rejected by isr_conv3x3_fwd
     }
+#ifdef ISR_TUNING
+    if (srow == -1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        conv_stamp(3, srow);
+    }
+#endif
 }
 
-template <class C>
-static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
-    if (d->cout % C::CT || d->cin % C::KC || d->ha % C::TH) return -2;
-    if (C::CIN && d->cin != C::CIN) return -2;
-    auto kern = conv3x3_fwd_kernel<C>;
+template <class C, bool XS2>
+__global__ __launch_bounds__(C::NT, C::OCC) void conv3x3_fwd_kernel(isr_conv_desc d) {
+    conv_tile<C, XS2, 0>(d, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+template <class C, bool XS2>
+static int launch3x3_k(const isr_conv_desc* d, hipStream_t s) {
+    auto kern = conv3x3_fwd_kernel<C, XS2>;
     lds_limit((const void*)kern, C::LDS);
     const int blocks = (d->wa / C::TW) * (d->ha / C::TH) * d->n * (d->cout / C::CT);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// FULL: the production tiles also carry the PixelShuffleᵀ-input form; the A/B variants
+// take the plain form only (x_sub2 → unsupported).
+template <class C, bool FULL = false>
+static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
+    if (d->cout % C::CT || d->cin % C::KC || d->ha % C::TH) return -2;
+    if (C::CIN && d->cin != C::CIN) return -2;
+    if constexpr (FULL) {
+        if (d->x_sub2) return launch3x3_k<C, true>(d, s);
+    } else {
+        if (d->x_sub2) return -2;
+    }
+    return launch3x3_k<C, false>(d, s);
 }
 
 // Variant table: variant 0 is the production choice per shape; the others are
@@ -511,93 +565,196 @@ static int launch3x3(const isr_conv_desc* d, hipStream_t s) {
 // cout == 32 (RDB growth convs)
 // V_G0 / V_F0: the next step's fragment reads interleaved one per MFMA (PIPE 2): 2-7 % over the
 // batched prefetch, whose 18-24 reads in flight exceed lgkmcnt's range (so hipcc waited lgkmcnt(0))
-using V_G0 = C3<4, 4, 1, 16, 2, 0, 0, 2>; // 16x32, 4 waves, KC16 double buffer, 64 KB → 2 blocks / CU
+using V_G0 = C3<4, 4, 1, 16, 2, 0, 0, 2>; // 16x32, 4 waves, KC16 double buffer, 58 KB → 2 blocks / CU
 using V_G1 = C3<4, 8, 1, 16, 3>; // 32x32 px tile, 8 waves, 3-deep KC16 ring
 using V_G2 = C3<2, 4, 1, 32, 2>; // 8x32, KC32, 2 blocks / CU
-using V_G3 = C3<2, 8, 1, 16, 3>; // 16x32, 8 waves x 2 rows, 3-deep KC16 ring
+using V_G3 = C3<2, 4, 1, 16, 2, 0, 0, 2>; // 8x32 tile, double buffer, interleaved
 // cout % 64 == 0
-using V_W0 = C3<4, 4, 2, 16, 2, 0, 0, 2>; // 16x32, 4 waves, KC16 double buffer, 80 KB → 2 blocks / CU, PIPE 2
+using V_W0 = C3<4, 4, 2, 16, 2, 0, 0, 2>; // 16x32, 4 waves, KC16 double buffer, 76 KB → 2 blocks / CU, PIPE 2
 using V_W1 = C3<4, 8, 2, 16, 2>; // 32x32 px tile, 8 waves, KC16 double buffer
 using V_W2 = C3<2, 4, 2, 32, 2>; // 8x32, KC32
-using V_W3 = C3<4, 4, 2, 32, 2>; // 16x32, KC32, 1 block / CU
+using V_W3 = C3<2, 4, 2, 16, 2, 0, 0, 2>; // 8x32 tile, interleaved
 using V_F0 = C3<4, 4, 2, 16, 2, 192, 0, 2>; // RDB final conv 192→64: V_W0 with compile-time cin, PIPE 2
 
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
     if (d->cout % 64) {  // 32-cout tiles: growth convs (cout 32) and dgrad of them (96, 160)
         switch (variant) {
-            case 0: return launch3x3<V_G0>(d, s);
+            case 0: return launch3x3<V_G0, true>(d, s);
             case 1: return launch3x3<V_G1>(d, s);
             case 2: return launch3x3<V_G2>(d, s);
             case 3: return launch3x3<V_G3>(d, s);
+            case 8: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 2, 4, 1>>(d, s);  // V_G0, refill before step-0 reads (r1)
+            case 9: return launch3x3<C3<4, 8, 1, 16, 2, 0, 0, 2>>(d, s);  // 32x32 tile, 8 waves, PIPE 2 (92 KB, 1 block/CU)
 #ifdef ISR_TUNING
             // ablations of V_G0 (timing only, outputs wrong): tuning builds only
             case 4: return launch3x3<C3<4, 4, 1, 16, 2, 0, 1>>(d, s);
             case 5: return launch3x3<C3<4, 4, 1, 16, 2, 0, 2>>(d, s);
             case 6: return launch3x3<C3<4, 4, 1, 16, 2, 0, 4>>(d, s);
             case 7: return launch3x3<C3<4, 4, 1, 16, 2, 0, 3>>(d, s);
-            case 16: return launch3x3<C3<4, 4, 1, 16, 2, 0, 32>>(d, s);  // probe: dx>0 activations by DPP shift
-            case 20: return launch3x3<C3<4, 4, 1, 16, 2, 0, 64>>(d, s);  // DVFS probe: 2x 16x16x32 per 32x32x16
 #endif
-            case 8: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 1>>(d, s);  // V_G0, one unit per epilogue pass
-            case 9: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 4, 2>>(d, s);  // V_G0, refill split over 2 steps
-            case 10: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 1, 4, 3>>(d, s); // V_G0, refill split over 3 steps
-            case 11: return launch3x3<C3<2, 4, 1, 16, 3>>(d, s);  // 8x32 tile, 3-deep ring (60 KB, 2 blocks/CU)
-            case 12: return launch3x3<C3<4, 4, 1, 16, 3>>(d, s);  // 16x32 tile, 3-deep ring (1 block/CU)
-            case 13: return launch3x3<C3<2, 4, 1, 16, 2>>(d, s);  // 8x32 tile, double buffer (3 blocks/CU)
-            case 14: return launch3x3<C3<4, 4, 1, 16, 2, 0, 8>>(d, s);   // V_G0, second block slot ~0.5 us late
-            case 15: return launch3x3<C3<4, 4, 1, 16, 2, 0, 16>>(d, s);  // V_G0, second block slot ~1 us late
-            case 17: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // V_G0, reads interleaved with MFMAs
-            case 18: return launch3x3<C3<4, 4, 1, 32, 2, 0, 0, 2>>(d, s);  // KC32 (1 block/CU), interleaved
-            case 19: return launch3x3<C3<2, 4, 1, 32, 2, 0, 0, 2>>(d, s);  // 8x32 KC32, interleaved
-            case 21: return launch3x3<C3<8, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // 32x32 tile, 8 rows per wave (1 block/CU)
-            case 22: return launch3x3<C3<8, 2, 1, 16, 2, 0, 0, 2>>(d, s);  // 16x32 tile, 2 waves x 8 rows
-            case 23: return launch3x3<C3<2, 8, 1, 16, 2, 0, 0, 2>>(d, s);  // 16x32 tile, 8 waves x 2 rows
-            case 24: return launch3x3<C3<2, 4, 1, 16, 2, 0, 0, 2>>(d, s);  // 8x32 tile, double buffer, interleaved
-            case 25: return launch3x3<C3<2, 4, 1, 16, 3, 0, 0, 2>>(d, s);  // 8x32 tile, 3-deep ring, interleaved
         }
         return -2;
     }
     switch (variant) {
-        case 0: return d->cin == 192 ? launch3x3<V_F0>(d, s) : launch3x3<V_W0>(d, s);
+        case 0: return d->cin == 192 ? launch3x3<V_F0, true>(d, s) : launch3x3<V_W0, true>(d, s);
         case 1: return launch3x3<V_W1>(d, s);
         case 2: return launch3x3<V_W2>(d, s);
         case 3: return launch3x3<V_W3>(d, s);
+        case 8: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 2, 4, 1>>(d, s)  // refill before reads (r1)
+                                     : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 2, 4, 1>>(d, s);
+        case 9: return d->cin == 192 ? launch3x3<C3<4, 8, 2, 16, 2, 192, 0, 2>>(d, s)  // 32x32, 8 waves, PIPE 2 (111 KB)
+                                     : launch3x3<C3<4, 8, 2, 16, 2, 0, 0, 2>>(d, s);
 #ifdef ISR_TUNING
         // ablations of V_W0 (timing only, outputs wrong): tuning builds only
         case 4: return launch3x3<C3<4, 4, 2, 16, 2, 0, 1>>(d, s);
         case 5: return launch3x3<C3<4, 4, 2, 16, 2, 0, 2>>(d, s);
         case 6: return launch3x3<C3<4, 4, 2, 16, 2, 0, 4>>(d, s);
         case 7: return launch3x3<C3<4, 4, 2, 16, 2, 0, 3>>(d, s);
-        case 16: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 32>>(d, s)  // probe: DPP-shifted dx>0
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 32>>(d, s);
-        case 20: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 64>>(d, s)  // DVFS probe (16x16x32)
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 64>>(d, s);
 #endif
-        case 8: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 0, 1>>(d, s)  // V_F0 / V_W0, one unit per pass
-                                     : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 1>>(d, s);
-        case 9: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 0, 4, 2>>(d, s)  // refill split over 2 steps
-                                     : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 2>>(d, s);
-        case 10: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 1, 4, 1>>(d, s)  // pipelined fragment reads
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 1, 4, 1>>(d, s);
-        case 11: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 1, 4, 2>>(d, s)  // both
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 1, 4, 2>>(d, s);
-        case 14: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 8>>(d, s)  // second block slot ~0.5 us late
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 8>>(d, s);
-        case 15: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 16>>(d, s)  // ~1 us late
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 16>>(d, s);
-        case 17: return d->cin == 192 ? launch3x3<C3<4, 4, 2, 16, 2, 192, 0, 2>>(d, s)  // reads interleaved with MFMAs
-                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 2>>(d, s);
-        case 18: return d->cin == 192 ? launch3x3<C3<2, 4, 2, 32, 2, 192, 0, 2>>(d, s)  // 8x32 KC32, interleaved
-                                      : launch3x3<C3<2, 4, 2, 32, 2, 0, 0, 2>>(d, s);
-        case 24: return d->cin == 192 ? launch3x3<C3<2, 4, 2, 16, 2, 192, 0, 2>>(d, s)  // 8x32 tile, interleaved
-                                      : launch3x3<C3<2, 4, 2, 16, 2, 0, 0, 2>>(d, s);
     }
     return -2;
 }
 
+// ============ persistent chain: a run of RDB convs in ONE launch ============
+// The RRDB trunk (utils/models.py:298-317, 245-271: per RDB four growth convs and the
+// final 192→64 conv) as one persistent launch instead of one launch per conv.  Every
+// layer shares the 16x32-pixel tile grid; workgroup b owns tiles b, b+G, ... for every
+// layer (all G workgroups resident: G <= 2 per CU, the kernel's occupancy).  Tile t of
+// layer L may start once tiles N(t) (itself and its 8 neighbours — the 3x3 halo) of layer
+// L-1 are done: their progress words reach L.  That single stencil dependency also covers
+// every older read/write hazard (a tile's layer-L-m ancestors within radius m are done).
+// Hand-off (cdna_hip_programming.md Guideline 16, R1): outputs are stored write-through
+// (sc1) and drained (s_waitcnt vmcnt(0) by every wave, barrier) before one lane publishes
+// the progress word with a relaxed agent-scope atomic store; consumers poll relaxed
+// (one lane per neighbour), then read the activations with sc1 loads (L1 bypass), and
+// with `acquire` additionally run one agent-scope acquire per tile first.
+// State (no per-call memset: a captured memset node was seen to leave garbage in the first
+// words under HIP-graph replay): state[0] = generation, bumped by a one-thread kernel ahead of
+// every chain launch; progress word of a tile = gen * 1024 + layers done (compared by serial-
+// number arithmetic, so it never needs zeroing); a bounded spin that gives up writes the
+// generation into state[1] (results invalid; the host checks state[1] == state[0]).
+struct ChainArgs {
+    const isr_conv_desc* layers;
+    const int32_t* kinds;
+    int nl, ntiles, nby, nbx;
+    unsigned* state;
+    int acquire;
+};
+
+#define CHAIN_STAMP_L0 75  // tuning stamps: the 15 layers of RRDB 5
+
+__global__ void chain_bump_kernel(unsigned* state) {
+    if (threadIdx.x == 0) state[threadIdx.x] = state[threadIdx.x] + 1u;  // vector store by lane 0
+}
+
+__device__ __forceinline__ void chain_wait(const ChainArgs& a, int t, unsigned need, unsigned gen) {
+    unsigned* progress = a.state + 4;
+    if (wave_id() == 0) {
+        const int lane = threadIdx.x & 63;
+        int nb = -1;
+        if (lane < 9) {
+            const int bx = t % a.nbx, by = (t / a.nbx) % a.nby, img = t / (a.nbx * a.nby);
+            const int yy = by + lane / 3 - 1, xx = bx + lane % 3 - 1;
+            if (yy >= 0 && yy < a.nby && xx >= 0 && xx < a.nbx) nb = (img * a.nby + yy) * a.nbx + xx;
+        }
+        for (unsigned spins = 0;; ++spins) {
+            const bool ok =
+                nb < 0 ||
+                (int)(__hip_atomic_load(progress + nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - need) >= 0;
+            if (__all(ok)) break;
+            // a neighbour never arrived (not resident?): give up after ~0.3 s, flag it, and let
+            // every later wait of the launch give up at once, so the grid always drains
+            if ((spins & 255) == 255 &&
+                __hip_atomic_load(a.state + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen)
+                break;
+            if (spins > (1u << 18)) {
+                if (lane == 0) __hip_atomic_store(a.state + 1, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (a.acquire) {
+            if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+}
+
+typedef const __attribute__((address_space(4))) isr_conv_desc const_desc;  // constant memory:
+// the host writes the layer table before the launch, so the compiler may re-load any field
+// (s_load) instead of holding it in registers across the tile
+
+// Static assignment: workgroup b owns tiles b, b+G, ... for every layer, so a tile's own
+// previous-layer outputs were written by the same CU.  A queue dealing (layer, tile) items in
+// layer order (no residency assumption) measured slower: 9.3 vs 6.8 ms per forward — it
+// rebuilds a per-layer front and loses that locality.  All G workgroups must be resident
+// (G <= 2 per CU); a wait that never completes gives up (bounded) instead of hanging.
+template <class CG, class CF>
+__global__ __launch_bounds__(256, 2) void conv_chain_kernel(ChainArgs a) {
+    // bumped by chain_bump_kernel before this launch; an agent-scope load, so no CU reads a
+    // stale copy of another XCD's write
+    const unsigned gen = __hip_atomic_load(a.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int L = 0; L < a.nl; ++L) {
+        const_desc& d = ((const_desc*)(uintptr_t)a.layers)[L];
+        const int kind = a.kinds[L];
+        for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+#ifdef ISR_TUNING
+            const int srow = (L >= CHAIN_STAMP_L0 && L < CHAIN_STAMP_L0 + 15) ? (L - CHAIN_STAMP_L0) * a.ntiles + t : -2;
+#else
+            const int srow = -2;
+#endif
+            conv_stamp(4, srow);  // wait start
+            if (L > 0) chain_wait(a, t, gen * 1024u + (unsigned)L, gen);
+            if (kind == 0) conv_tile<CG, false, 1>(d, t, srow);
+            else conv_tile<CF, false, 1>(d, t, srow);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores are done
+            conv_stamp(3, srow);
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(a.state + 4 + t, gen * 1024u + (unsigned)(L + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+size_t conv_chain_state_words(int n, int ha, int wa) {
+    const size_t tiles = (size_t)n * (ha / V_G0::TH) * (wa / V_G0::TW);
+    return (tiles + 4 + 3) / 4 * 4;  // [0] fail word, [4..] progress; a multiple of 16 bytes
+}
+
+int conv_chain(const isr_chain_desc* c, hipStream_t s) {
+    static_assert(V_G0::TH == V_F0::TH && V_G0::TW == V_F0::TW, "one tile grid");
+    static_assert(V_G0::NT == 256 && V_F0::NT == 256, "chain block size");
+    ChainArgs a;
+    a.layers = c->layers;
+    a.kinds = c->kinds;
+    a.nl = c->nl;
+    a.nby = c->ha / V_G0::TH;
+    a.nbx = c->wa / V_G0::TW;
+    a.ntiles = c->n * a.nby * a.nbx;
+    a.state = c->state;
+    a.acquire = c->acquire;
+    if (c->nl >= 1024) return -2;
+    hipLaunchKernelGGL(chain_bump_kernel, dim3(1), dim3(64), 0, s, c->state);
+    auto kern = conv_chain_kernel<V_G0, V_F0>;
+    constexpr int lds = V_G0::LDS > V_F0::LDS ? V_G0::LDS : V_F0::LDS;
+    lds_limit((const void*)kern, lds);
+    const int slots = 2 * cu_count();  // every workgroup resident: 2 per CU (the kernel's occupancy)
+    const int grid = a.ntiles < slots ? a.ntiles : slots;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+#ifdef ISR_TUNING
+int conv_stamps_set(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_conv_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+#else
+int conv_stamps_set(void*) { return -2; }
+#endif
+
 int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) {
-    if (d->taps == 1) return d->cout % 64 ? -2 : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 1, 1>>(d, s);
-    if (d->taps == 2) return d->cout % 64 ? -2 : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 1, 2>>(d, s);
+    if (d->taps == 1) return d->cout % 64 ? -2 : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 1, 1>, true>(d, s);
+    if (d->taps == 2) return d->cout % 64 ? -2 : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 1, 2>, true>(d, s);
     return conv3x3_fwd_variant(d, 0, s);
 }
 

@@ -35,6 +35,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds) {
     __builtin_amdgcn_global_load_lds(gsrc, ISR_LDS_PTR(lds), 16, 0, 0);
 }
 
+// The same copy with sc1 (bypasses this CU's L1): reads of activations another workgroup
+// of the same launch wrote (cdna_hip_programming.md Guideline 16 hand-offs).
+__device__ __forceinline__ void glds16_sc1(const void* gsrc, void* lds) {
+    __builtin_amdgcn_global_load_lds(gsrc, ISR_LDS_PTR(lds), 16, 0, 16);
+}
+
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ int wave_id() {
@@ -44,7 +50,8 @@ __device__ __forceinline__ int wave_id() {
 // Activations are channel-blocked: [N][cs/16][hp][wp][16] bf16 (one 16-channel
 // "plane" per block of channels).  Byte address of interior pixel (img, y, x),
 // view channel c (c % 8 == 0 for vector accesses).
-__device__ __forceinline__ char* view_at(const isr_view& v, int img, int y, int x, int c) {
+template <class V>
+__device__ __forceinline__ char* view_at(const V& v, int img, int y, int x, int c) {
     const int ch = v.coff + c;
     const size_t plane = (size_t)img * (v.cs >> 4) + (ch >> 4);
     const size_t pix = (plane * v.hp + (y + v.pad)) * (size_t)v.wp + (size_t)(x + v.pad);
@@ -52,7 +59,8 @@ __device__ __forceinline__ char* view_at(const isr_view& v, int img, int y, int 
 }
 
 // Byte stride between consecutive 16-channel planes of a view.
-__device__ __forceinline__ size_t plane_bytes(const isr_view& v) { return (size_t)v.hp * v.wp * 32; }
+template <class V>
+__device__ __forceinline__ size_t plane_bytes(const V& v) { return (size_t)v.hp * v.wp * 32; }
 
 // Bijective XCD-aware remap of a 1D block id: blocks b and b+8 run on the same
 // XCD (round-robin dispatch, MI355X_MICROARCH.md), so give each XCD a
@@ -79,6 +87,41 @@ __device__ __forceinline__ void store8_bf16(char* p, const float* v) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) t[e] = (__bf16)v[e];
     *reinterpret_cast<bf16x8*>(p) = t;
+}
+
+// 16-byte load / 8-channel bf16 store at `p` inside view `v`: plain (HX = 0), or the hand-off
+// form (HX = 1: sc1 load that bypasses L1; write-through sc1 store, Guideline 16 R1) through a
+// buffer descriptor built from the view's base (wave-uniform: no waterfall) with the byte
+// offset as the per-lane voffset — hand-off buffers are far below the 2 GiB window.
+template <class V>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const V& v) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(v.data), (short)0, 0x7fffffff, 0x00020000);
+}
+
+template <int HX, class V>
+__device__ __forceinline__ bf16x8 load16_hx(const V& v, const char* p) {
+    if constexpr (HX) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+        const int off = (int)(p - (const char*)v.data);
+        u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(v), off, 0, 16);
+        return __builtin_bit_cast(bf16x8, r);
+    } else {
+        return *reinterpret_cast<const bf16x8*>(p);
+    }
+}
+
+template <int HX, class V>
+__device__ __forceinline__ void store8_bf16_hx(const V& v, char* p, const float* x) {
+    bf16x8 t;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = (__bf16)x[e];
+    if constexpr (HX) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+        const int off = (int)(p - (const char*)v.data);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), rsrc_of(v), off, 0, 16);
+    } else {
+        *reinterpret_cast<bf16x8*>(p) = t;
+    }
 }
 
 // Fused epilogue on 8 consecutive output channels [co, co+8) of one pixel.

@@ -147,9 +147,12 @@ class GeneratorPlan:
     """
 
     def __init__(self, gw: GeneratorWeights, n: int, h: int, w: int, device, x_u8: bool, out_u8: bool,
-                 mean, std, variants: dict | None = None):
+                 mean, std, variants: dict | None = None, chain: bool | None = None, chain_acquire: bool = False):
         """`variants` (tuning only) maps ("conv3x3", cin, cout) or ("conv3x3", "*", cout)
-        to an isr_conv3x3_fwd_variant id; unlisted convs use the production kernel."""
+        to an isr_conv3x3_fwd_variant id; unlisted convs use the production kernel.
+        `chain` (default CHAIN_DEFAULT): the RRDB trunk as one persistent isr_conv_chain launch."""
+        if chain is None:
+            chain = CHAIN_DEFAULT
         self.key = (n, h, w, str(device), x_u8, out_u8, tuple(mean), tuple(std))
         bufs = GeneratorBuffers(n, h, w, len(gw.scalers), device)
         self.bufs = bufs
@@ -173,12 +176,19 @@ class GeneratorPlan:
             L.append((conv, ops.conv3x3_desc(src, pc.cin, pc.w, pc.b, pc.cout, dst, **kw), tag, v))
 
         ar = gw.add_rate
+        trunk0 = len(L)
         for blk in gw.rdb:
             for r, (src, dst) in enumerate(((X, Y), (Y, Z), (Z, X))):
                 for k in range(4):
                     c3(src, blk[r][k], src, y_coff=blk[r][k].cin, slope=LEAKY_DEFAULT)
                 extra = dict(r2=X, s2=ar) if r == 2 else {}
                 c3(src, blk[r][4], dst, slope=1.0, r1=src, s1=ar, **extra)
+        self.chain = None
+        if chain and gw.rdb and not variants:
+            # the whole RRDB trunk as ONE persistent launch (isr_conv_chain): tile-level
+            # dependencies instead of 240 kernel boundaries
+            self.chain = ConvChain([d for _, d, _, _ in L[trunk0:]], X, device, acquire=chain_acquire)
+            L[trunk0:] = [(self.chain.fn, self.chain.desc, ("chain", len(L) - trunk0), None)]
         c3(X, gw.conv1, feat, slope=1.0, r1=feat, s1=1.0)
         cur = feat
         for s, pc in enumerate(gw.scalers):
@@ -216,6 +226,43 @@ class GeneratorPlan:
         return out
 
 
+class ConvChain:
+    """Device-side layer table + state for isr_conv_chain over a run of RDB convs
+    (growth convs: kind 0; 192→64 final convs: kind 1) sharing one tile grid."""
+
+    def __init__(self, descs, grid: ActBuffer, device, acquire: bool = False):
+        lib = ops._lib.load()
+        kinds = []
+        for d in descs:
+            ops.check(lib.isr_conv3x3_check(ctypes.byref(d)), "chain layer")
+            if d.cout == 32:
+                kinds.append(0)
+            elif d.cin == 192 and d.cout == 64:
+                kinds.append(1)
+            else:
+                raise ValueError(f"conv chain: unsupported layer {d.cin}->{d.cout}")
+            if d.x_sub2 or d.taps or d.shuffle != 1 or d.m.data or d.y2.data:
+                raise ValueError("conv chain: plain 3x3 layers only")
+            if (d.n, d.ha, d.wa) != (grid.n, grid.ha, grid.wa):
+                raise ValueError("conv chain: every layer must share the tile grid")
+        if grid.t.numel() * 2 >= 2 ** 31:
+            raise ValueError("conv chain: activation buffers must stay below 2 GiB (buffer-descriptor window)")
+        raw = b"".join(bytes(d) for d in descs)
+        self._table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        self._kinds = torch.tensor(kinds, dtype=torch.int32, device=device)
+        words = lib.isr_conv_chain_state_words(grid.n, grid.ha, grid.wa)
+        self.state = torch.zeros(words, dtype=torch.int32, device=device)
+        self.desc = ops._lib.IsrChainDesc(self._table.data_ptr(), self._kinds.data_ptr(), len(descs), grid.n,
+                                          grid.ha, grid.wa, self.state.data_ptr(), int(acquire))
+        self.fn = lib.isr_conv_chain
+        self.nl = len(descs)
+
+    def failed(self) -> bool:
+        """True when a dependency wait gave up in the last launch (results invalid)."""
+        gen, fail = self.state[:2].tolist()
+        return gen != 0 and fail == gen
+
+
 class SplitGeneratorPlan:
     """The batch split into `splits` equal sub-batches, each with its own buffers
     and launch list on its own HIP stream; launches are issued interleaved
@@ -224,13 +271,14 @@ class SplitGeneratorPlan:
     beside another's main loop (MFMA-bound) on the same CUs."""
 
     def __init__(self, gw: GeneratorWeights, n: int, h: int, w: int, device, x_u8: bool, out_u8: bool,
-                 mean, std, splits: int = 2, stagger_us: float = 0.0, variants: dict | None = None):
+                 mean, std, splits: int = 2, stagger_us: float = 0.0, variants: dict | None = None,
+                 chain: bool | None = None):
         if n % splits:
             raise ValueError(f"batch {n} does not split into {splits} equal sub-batches")
         self.m = n // splits
         self.key = (n, h, w, str(device), x_u8, out_u8, tuple(mean), tuple(std), splits, stagger_us)
-        self.subs = [GeneratorPlan(gw, self.m, h, w, device, x_u8, out_u8, mean, std, variants=variants)
-                     for _ in range(splits)]
+        self.subs = [GeneratorPlan(gw, self.m, h, w, device, x_u8, out_u8, mean, std, variants=variants,
+                                   chain=chain) for _ in range(splits)]
         self.out_shape = (n,) + self.subs[0].out_shape[1:]
         self.out_dtype = self.subs[0].out_dtype
         self.streams = [torch.cuda.Stream(device) for _ in range(splits)]
@@ -280,6 +328,11 @@ def _sleep_cycles_per_us() -> float:
     return _SLEEP_CAL[0]
 
 
+# The RRDB trunk runs as one persistent isr_conv_chain launch by default (ISR_CHAIN=0:
+# one launch per conv).
+import os as _os
+CHAIN_DEFAULT = _os.environ.get("ISR_CHAIN", "0") == "1"
+
 # Batches of >= 2 (even) are split over this many HIP streams by default: two
 # half-batch launch lists run concurrently, so one stream's kernel tail, prologue
 # and HBM-bound epilogue overlap the other's MFMA main loop (+6 % on the
@@ -312,24 +365,26 @@ class GraphedPlan:
 
 
 def make_plan(gw: GeneratorWeights, n: int, h: int, w: int, device, x_u8: bool, out_u8: bool, mean, std,
-              streams: int | None = None):
-    """GeneratorPlan, or a SplitGeneratorPlan over `streams` (default DEFAULT_STREAMS)
-    HIP streams when the batch divides evenly."""
-    k = DEFAULT_STREAMS if streams is None else streams
+              streams: int | None = None, chain: bool | None = None):
+    """GeneratorPlan, or a SplitGeneratorPlan over `streams` (default DEFAULT_STREAMS, or 1
+    with the chained trunk) HIP streams when the batch divides evenly."""
+    chain = CHAIN_DEFAULT if chain is None else chain
+    k = (1 if chain else DEFAULT_STREAMS) if streams is None else streams
     if k > 1 and n >= k and n % k == 0:
-        return SplitGeneratorPlan(gw, n, h, w, device, x_u8, out_u8, mean, std, splits=k)
-    return GeneratorPlan(gw, n, h, w, device, x_u8, out_u8, mean, std)
+        return SplitGeneratorPlan(gw, n, h, w, device, x_u8, out_u8, mean, std, splits=k, chain=chain)
+    return GeneratorPlan(gw, n, h, w, device, x_u8, out_u8, mean, std, chain=chain)
 
 
-def get_plan(gw: GeneratorWeights, x: torch.Tensor, out_u8: bool, mean, std, streams: int | None = None):
+def get_plan(gw: GeneratorWeights, x: torch.Tensor, out_u8: bool, mean, std, streams: int | None = None,
+             chain: bool | None = None):
     n, c, h, w = x.shape
     if c != 3:
         raise ValueError(f"generator expects 3 input channels, got {c}")
-    key = (n, h, w, str(x.device), x.dtype == torch.uint8, out_u8, tuple(mean), tuple(std), streams)
+    key = (n, h, w, str(x.device), x.dtype == torch.uint8, out_u8, tuple(mean), tuple(std), streams, chain)
     plan = gw.buffers.get("plan")
     if plan is None or gw.buffers.get("plan_key") != key:
         gw.buffers["plan"] = None  # free the previous geometry first
-        plan = make_plan(gw, n, h, w, x.device, x.dtype == torch.uint8, out_u8, mean, std, streams)
+        plan = make_plan(gw, n, h, w, x.device, x.dtype == torch.uint8, out_u8, mean, std, streams, chain)
         gw.buffers["plan"] = plan
         gw.buffers["plan_key"] = key
     return plan

@@ -310,6 +310,37 @@ int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s);
  * ablations exist only in a library built with -DISR_TUNING.  Returns
  * ISR_ERR_UNSUPPORTED for an unknown variant. */
 int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_t s);
+/* Tuning builds (-DISR_TUNING) only: per-block wall-clock stamps of later conv3x3
+ * launches into `buf` (8 x uint64 per block: entry, first chunk landed, main loop
+ * done, epilogue done [s_memrealtime, 100 MHz], -, -, HW_ID, XCC_ID); NULL stops.
+ * A default build returns ISR_ERR_UNSUPPORTED. */
+int isr_tuning_conv_stamps(void* buf);
+/* Validation only: ISR_OK when isr_conv3x3_fwd would accept `d` (nothing launched). */
+int isr_conv3x3_check(const isr_conv_desc* d);
+
+/* Persistent chain of RDB convs (the RRDB trunk, utils/models.py:245-317) in ONE launch:
+ * layer i is layers[i] (device memory), each a descriptor isr_conv3x3_check accepts, of
+ * kind kinds[i]: 0 = growth conv (cout 32), 1 = RDB final conv (cin 192, cout 64); all
+ * layers share n, ha, wa (plain 3x3, no x_sub2 / taps / shuffle / mask).  Replaces nl
+ * isr_conv3x3_fwd calls with the same outputs.  Tiles of layer i start as soon as their
+ * 3x3 tile neighbourhood of layer i-1 is done (tile-level dependencies, no grid barrier).
+ * `state` (device, isr_conv_chain_state_words(n, ha, wa) uint32 words, zeroed ONCE by the
+ * caller before first use, then owned by the library across calls: a generation counter in
+ * state[0] replaces per-call zeroing); after a call, state[1] == state[0] means a dependency
+ * wait gave up (results invalid — not expected unless the device is shared).  nl < 1024.
+ * acquire = 1 adds an agent-scope acquire before each tile's loads (otherwise the
+ * hand-off relies on sc1 loads). */
+typedef struct isr_chain_desc {
+    const isr_conv_desc* layers;
+    const int32_t* kinds;
+    int32_t nl;
+    int32_t n, ha, wa;
+    uint32_t* state;
+    int32_t acquire;
+} isr_chain_desc;
+size_t isr_conv_chain_state_words(int32_t n, int32_t ha, int32_t wa);
+int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
+
 int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s);
 int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);
 /* Tuning / A-B entry point: 0 = production (= 3), 1 = one tile per block, 3 = one 8-row tile per block (76 KB LDS, 2 blocks / CU), 2 = persistent

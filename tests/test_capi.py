@@ -36,6 +36,7 @@ PROBE = r"""
 #include <stddef.h>
 #include "isr.h"
 #define F(s, m) printf(#s "." #m " %zu\n", offsetof(s, m))
+#define S(s) printf(#s " %zu\n", sizeof(s))
 int main(void) {
   printf("isr_view %zu\nisr_conv_desc %zu\nisr_head_desc %zu\nisr_tail_desc %zu\n",
          sizeof(isr_view), sizeof(isr_conv_desc), sizeof(isr_head_desc), sizeof(isr_tail_desc));
@@ -43,6 +44,8 @@ int main(void) {
   F(isr_conv_desc, bias); F(isr_conv_desc, slope); F(isr_conv_desc, shuffle);
   F(isr_head_desc, x); F(isr_head_desc, x_u8); F(isr_head_desc, inv_std); F(isr_head_desc, y);
   F(isr_head_desc, slope); F(isr_tail_desc, x); F(isr_tail_desc, y); F(isr_tail_desc, y_u8);
+  S(isr_chain_desc); F(isr_chain_desc, kinds); F(isr_chain_desc, nl); F(isr_chain_desc, wa);
+  F(isr_chain_desc, state); F(isr_chain_desc, acquire);
   return 0;
 }
 """
@@ -55,11 +58,12 @@ def test_struct_layouts_match_c(tmp_path):
     subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
     c = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True).stdout.splitlines())
     py = {"isr_view": ctypes.sizeof(_lib.IsrView), "isr_conv_desc": ctypes.sizeof(_lib.IsrConvDesc),
-          "isr_head_desc": ctypes.sizeof(_lib.IsrHeadDesc), "isr_tail_desc": ctypes.sizeof(_lib.IsrTailDesc)}
+          "isr_head_desc": ctypes.sizeof(_lib.IsrHeadDesc), "isr_tail_desc": ctypes.sizeof(_lib.IsrTailDesc),
+          "isr_chain_desc": ctypes.sizeof(_lib.IsrChainDesc)}
     for k, v in py.items():
         assert int(c[k]) == v, k
     cls = {"isr_view": _lib.IsrView, "isr_conv_desc": _lib.IsrConvDesc, "isr_head_desc": _lib.IsrHeadDesc,
-           "isr_tail_desc": _lib.IsrTailDesc}
+           "isr_tail_desc": _lib.IsrTailDesc, "isr_chain_desc": _lib.IsrChainDesc}
     for key, val in c.items():
         if "." in key:
             s, m = key.split(".")

@@ -1,0 +1,68 @@
+"""The persistent RRDB-trunk kernel (isr_conv_chain, conv3x3.hip): the whole trunk of
+RDB convs in one launch with tile-level dependencies must reproduce the per-conv
+launches BIT FOR BIT (same tile arithmetic; only the hand-off differs: sc1 loads /
+write-through stores, progress words).  Repeated launches stress the hand-off for
+races or stale reads; several geometries cover ragged tiles and more tiles than
+resident workgroups (a workgroup walking several tiles per layer)."""
+import pytest
+import torch
+
+from image_super_resolution_amd import engine, models
+from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_state_dict
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib(built_lib):
+    return built_lib
+
+
+def _gw(blocks, scale=4, enchant=False, seed=0):
+    m = (models.EResNet if enchant else models.ResNet)(blocks, 0.2, scaleRate=scale)
+    sd = synth_state_dict(m.state_dict(), seed)
+    return engine.pack_generator({k: v.to(DEV) for k, v in sd.items()}, enchant=enchant, device=DEV)
+
+
+def _run(gw, xs, chain, acquire=False):
+    """One plan, one forward per input in `xs` (different inputs back to back: a stale
+    hand-off read would return the previous input's activations and show up)."""
+    x0 = xs[0]
+    plan = engine.GeneratorPlan(gw, x0.shape[0], x0.shape[2], x0.shape[3], x0.device, False, False,
+                                (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), chain=chain, chain_acquire=acquire)
+    outs = []
+    for x in xs:
+        out = torch.empty(plan.out_shape, device=DEV)
+        plan.run(x, out)
+        outs.append(out)
+    torch.cuda.synchronize()
+    if chain:
+        assert plan.chain is not None and not plan.chain.failed(), "a chain dependency wait gave up"
+    return outs
+
+
+def _inputs(n, h, w, k, seed):
+    return [normalize(synth_lr_batch(n, h, w, seed=seed + i, scale=4)[0]).to(DEV).contiguous() for i in range(k)]
+
+
+@pytest.mark.parametrize("n,h,w,blocks", [(2, 36, 52, 2), (1, 128, 128, 1), (16, 128, 128, 16), (4, 256, 256, 2)])
+def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks):
+    gw = _gw(blocks)
+    xs = _inputs(n, h, w, 3, seed=3)
+    refs = _run(gw, xs, chain=False)
+    for acquire in (False, True):
+        for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire), refs):
+            assert torch.equal(out, ref), f"chain (acquire={acquire}) differs: max {(out - ref).abs().max().item()}"
+
+
+def test_chain_repeated_stress_eresnet():
+    """EResNet (no BN; conv weights scaled 0.2): 20 back-to-back chained forwards at the
+    bench shape over 4 different inputs in turn, every output bitwise equal to the
+    per-conv launches of the same input."""
+    gw = _gw(4, enchant=True, seed=2)
+    xs = _inputs(16, 128, 128, 4, seed=9)
+    refs = _run(gw, xs, chain=False)
+    for _ in range(5):
+        for out, ref in zip(_run(gw, xs, chain=True), refs):
+            assert torch.equal(out, ref)
