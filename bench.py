@@ -12,21 +12,22 @@ collective on the data path; only the timing uses a MAX all-reduce).
 Prints one JSON line (rank 0).  The timed steps replay the forward as one HIP
 graph (engine.GraphedPlan; --no-graph for the eager ctypes launch loop, whose
 ~15 us of host time per launch would otherwise bound the step).  Extra fields:
-  roofline      — the dominant kernel: the RDB growth conv (conv3x3_fwd with a
-                  32-cout tile, 4 x 48 launches per forward, the largest share
-                  of the step), against the HBM bound.  Algorithmic bytes per
-                  launch = (cin + 32) channels x 2 B x N*H*W (input read once,
-                  output written once; weights < 0.1 %), averaged over the four
-                  growth shapes (cin 64/96/128/160).  Its 192 launches of one
-                  forward are replayed back to back on the launch stream between
-                  one pair of HIP events (5 rounds, median; single-stream
-                  full-batch plan), so the per-launch average matches rocprofv3's
-                  kernel trace of the same command.  traffic = PMC HBM bytes per
-                  launch of that kernel from profiles/<round>_pmc_traffic.json
+  roofline      — the dominant kernel: the persistent RRDB-trunk kernel
+                  (isr_conv_chain: all 240 RDB convs in one launch, ~85 % of the
+                  step), against the HBM bound (the trunk's layer-
+                  granularity bytes bind, B/BW > F/P).  Algorithmic bytes per launch
+                  = 48 RDBs x (each conv's input read once + output written once:
+                  832 channels) x 2 B x N*H*W = 20.9 GB at N=16, 128²; its launch is
+                  replayed back to back on the launch stream between one pair of HIP
+                  events (5 rounds, median), so the per-launch time matches
+                  rocprofv3's kernel trace of the same command.  traffic = PMC HBM
+                  bytes per launch from profiles/<round>_pmc_traffic.json
                   (rocprofv3 --pmc, corrected per MI355X_MICROARCH.md), or null.
-  roofline_kernels — the same measurement for both conv templates, each against
-                  its own bound: growth (HBM) and the RDB final conv 192->64
-                  (MFMA, 2*9*192*64 FLOP per output pixel).
+  roofline_kernels — the chain kernel, and the per-conv kernels it is built from
+                  (used by the training path and the non-chained plan), each against
+                  its own bound: growth convs (32-cout tile, HBM: (cin + 32) channels x
+                  2 B x N*H*W per launch) and the RDB final conv 192->64 (MFMA,
+                  2*9*192*64 FLOP per output pixel), timed on a per-conv plan.
   model_roofline — SURVEY.md §8d: max(F / P_mfma, B / BW_hbm) / t_step for the
                   whole forward (F = 410.9 GFLOP and B = 1.403 GB bf16 per 128²
                   tile at layer granularity).
@@ -184,16 +185,33 @@ def main():
     ms = elapsed / args.steps * 1e3
     hr_px = n * (hw * S) * (hw * S)
     mpix_s = world * hr_px * args.steps / elapsed / 1e6
-    # Per-kernel roofline: each conv template's launches of one forward replayed back to
-    # back on a single-stream full-batch plan (under the split plan two half-batch
-    # launches share the CUs, so a launch's duration is not its own); after the timed region.
-    iso = plan if n_streams == 1 else engine.GeneratorPlan(gw, n, hw, hw, dev, False, False, mean, std)
-    iso.run(x, out)
-    torch.cuda.synchronize()
+    # Per-kernel roofline, after the timed region.  The production forward's dominant kernel
+    # is the persistent trunk kernel (isr_conv_chain, all 240 RDB convs): its launch replayed
+    # back to back on the launch stream between HIP events.  The per-conv kernels (used by the
+    # training path and the non-chained plan) are timed the same way on a single-stream,
+    # full-batch, per-conv plan (under a split plan two half-batch launches share the CUs, so
+    # a launch's duration is not its own).
     stream, sp = torch.cuda.current_stream(), ops._stream()
     npx = n * hw * hw
     traffic = load_traffic(args.round)
     kernels = {}
+    chained = (plan.subs[0] if n_streams > 1 else plan).chain is not None
+    if chained and n_streams == 1:
+        c_ms, c_tags = time_family(plan, {("chain", 15 * args.blocks)}, stream, sp)
+        trunk_bytes = args.blocks * 3 * (sum(64 + 32 * k + 32 for k in range(4)) + 192 + 64) * 2 * npx
+        trunk_flops = args.blocks * 3 * (sum(2.0 * 9 * (64 + 32 * k) * 32 for k in range(4))
+                                         + 2.0 * 9 * 192 * 64) * npx
+        c_gbs = trunk_bytes / (c_ms * 1e-3) / 1e9
+        kernels["chain"] = {"bound": "hbm", "kernel": "conv_chain_kernel (RRDB trunk: 240 convs, one persistent launch)",
+                            "achieved": round(c_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(c_gbs / HBM_PEAK_GBS, 4), "traffic": traffic.get("chain"),
+                            "bytes_per_launch": trunk_bytes, "flops_per_launch": trunk_flops,
+                            "avg_launch_ms": round(c_ms, 5), "launches_per_step": len(c_tags),
+                            "mfma_frac": round(trunk_flops / (c_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+                            "share_of_step": round(c_ms / ms, 4)}
+    iso = engine.GeneratorPlan(gw, n, hw, hw, dev, False, False, mean, std, chain=False)
+    iso.run(x, out)
+    torch.cuda.synchronize()
     g_ms, g_tags = time_family(iso, GROWTH, stream, sp)
     g_bytes = statistics.mean((t[1] + t[2]) * 2 * npx for t in g_tags)
     g_flops = statistics.mean(2.0 * 9 * t[1] * t[2] * npx for t in g_tags)
@@ -272,8 +290,9 @@ def main():
                                    f"{hw}x{hw}->{hw * S}x{hw * S}",
                        "global_batch": n * world, "per_gpu_batch": n, "lr_size": hw, "scale": S,
                        "parallelism": f"dp{world} (independent tile shards)",
-                       "streams_per_gpu": n_streams, "hip_graph": not args.no_graph},
-            "roofline": kernels["growth"],
+                       "streams_per_gpu": n_streams, "hip_graph": not args.no_graph,
+                       "trunk": "persistent chain kernel" if chained else "one launch per conv"},
+            "roofline": kernels.get("chain", kernels["growth"]),
             "roofline_kernels": kernels,
             "model_roofline": model_roofline,
             "model_tflops_per_s": round(model_flops / (ms * 1e-3) / 1e12, 2),

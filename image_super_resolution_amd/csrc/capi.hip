@@ -11,6 +11,7 @@ namespace isr {
 int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s);
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s);
 int conv_stamps_set(void* p);
+int tail_stamps_set(void* p);
 size_t conv_chain_state_words(int n, int ha, int wa);
 int conv_chain(const isr_chain_desc* c, hipStream_t s);
 size_t conv3x3_packed_bytes(int cout, int cin);
@@ -235,6 +236,12 @@ int isr_tuning_conv_stamps(void* buf) {
     const int rc = isr::conv_stamps_set(buf);
     if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "conv stamps: library built without -DISR_TUNING");
     return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "conv stamps: hipMemcpyToSymbol failed");
+}
+
+int isr_tuning_tail_stamps(void* buf) {
+    const int rc = isr::tail_stamps_set(buf);
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "tail stamps: library built without -DISR_TUNING");
+    return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "tail stamps: hipMemcpyToSymbol failed");
 }
 
 int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_t s) {

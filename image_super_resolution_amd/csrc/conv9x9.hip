@@ -591,6 +591,283 @@ __global__ __launch_bounds__(256, 1) void tail9x9_pkernel(isr_tail_desc d, int n
     }
 }
 
+// ---- row-streaming tail (variant 4): no recomputed rows.  A block owns a 32-column strip of
+// one image over `sh` output rows and walks DOWN it: each wave turns one input row into its
+// T row (the 1x9 row conv, N = (ky, co)) with 36 MFMAs, every T row is computed once (the
+// per-tile kernels recompute the 8 halo rows of every tile: 2x the MFMA work at 8-row tiles),
+// and output row y is finished once T rows y-4 .. y+4 exist.  Input rows stream through a
+// 3-group LDS ring (4 rows per group, two groups in flight); the T terms go to a 16-row ring
+// keyed by the output row they feed (O[r0][px][pos(co, ky)] = T(r0+ky)[px][ky*3+co]).
+// The 36 weight fragments stay in VGPRs (one LDS read per MFMA instead of two: with weights
+// in LDS the four waves' fragment reads saturated the LDS port before the MFMAs did).  One
+// wave per SIMD, so the finish of an older output row (T reads, ky sums, tanh, 2 stores) is
+// interleaved into the MFMA sequence of the current T row.  Same MFMA order per T element and
+// the same ky-sum order as the per-tile kernels: bit-identical outputs.
+// LDS reads of the loop are asm (lds_read16_async / lds_read16f4_async) with counted lgkmcnt
+// waits: hipcc's own waits here were lgkmcnt(0) every few MFMAs.  Counted vmcnt: per wave,
+// 5 LDS-DMA per row group and exactly 2 stores per finished row.
+namespace tails {
+constexpr int TW = 32, WM = 4, GR = 4;       // strip width, waves, rows per group (one per wave)
+constexpr int HC = TW + 8;                    // 40 input columns per row
+constexpr int ROWB = 4 * HC * 32;             // one input row image: 4 planes x 40 px x 32 B = 5120
+constexpr int ROW_INSTR = ROWB / 1024;        // 5
+constexpr int NG = 3;                         // input row groups in the ring
+constexpr int NT = 16;                        // O ring rows: read 4i-16 .. 4i-13 while writing 4i-12 .. 4i-1
+constexpr int TS = 36;                        // O row: [px][co 0: 0..8, co 1: 9..17, co 2: 20..28] + pad
+constexpr int TROW = TW * TS * 4;             // 4608 (TS = 36: conflict-free 16-B px reads)
+constexpr int OFF_IN = 0;
+constexpr int OFF_T = OFF_IN + NG * GR * ROWB;      // 61440
+constexpr int LDS = OFF_T + NT * TROW;             // 135168
+constexpr int PD = 6;                          // A-fragment prefetch distance (MFMA steps)
+constexpr int ST = 2;                          // stores per finished row per wave
+static_assert(LDS <= 163840, "LDS");
+}  // namespace tails
+
+__device__ __forceinline__ f32x4 lds_read16f4_async(const char* p) {
+    f32x4 r;
+    const uint32_t a = (uint32_t)(uintptr_t)ISR_LDS_PTR(p);
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a) : "memory");
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void lds_wait_t(bf16x8& a, f32x4 (&t)[5]) {
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(a), "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4])
+                 : "i"(N));
+}
+template <int N>
+__device__ __forceinline__ void lds_wait_t4(f32x4 (&t)[5]) {
+    asm volatile("s_waitcnt lgkmcnt(%5)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4])
+                 : "i"(N));
+}
+template <int N>
+__device__ __forceinline__ void lds_wait1(bf16x8& a) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(N));
+}
+__device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n a small runtime-uniform value
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+#ifdef ISR_TUNING
+__device__ unsigned long long* g_tail_stamps;  // isr_tuning_tail_stamps
+#endif
+__device__ __forceinline__ unsigned long long rt_now() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+// ABL (tuning builds only, outputs wrong): 1 no MFMA, 2 no output-row finish, 4 no row DMA in the
+// loop; 16 (outputs right) per-wave s_memrealtime sums: [entry, exit, top wait + barrier, loop]
+//
+// Schedule of iteration i (wave w), one wave per SIMD so every side job rides in the gaps of
+// the 36-MFMA chain of T row 4i+w (one A-fragment read per gap, PD steps ahead):
+//   gaps 1..5    LDS-DMA of row group i+2 (one 1-KB copy per gap)
+//   gaps 6..21   O-ring writes of T row 4(i-1)+w (the previous iteration's accumulator)
+//   gaps 1..9    ky sums of output row 4(i-4)+w (its O-ring terms read before the prefetch)
+//   gaps 12, 24  tanh + store of its two channel slots
+// so a T row is written one iteration after it is computed and read one iteration later.
+template <int ABL>
+__global__ __launch_bounds__(256, 1) void tail9x9_stream_kernel(isr_tail_desc d, int sh) {
+    using namespace tails;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nstrip = d.wa / TW, nseg = d.ha / sh;
+    int b = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring strips (shared halo columns) on one XCD
+    const int strip = b % nstrip;
+    b /= nstrip;
+    const int seg = b % nseg;
+    const int img = b / nseg;
+    const int x0 = strip * TW, ys = seg * sh;
+    const int wave = wave_id();
+    const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+    const int nit = sh / GR + 2;  // T rows ys-4 .. ys+sh+3, four per iteration
+    float* T = reinterpret_cast<float*>(smem + OFF_T);
+    const size_t pstride = plane_bytes(d.x);
+    const char* xcol = view_at(d.x, img, 0, x0 - 4, 0);  // row 0 of the strip's input columns
+    const int xrow = d.x.wp * 32;
+
+    // LDS-DMA of row group g (T rows ys-4+4g .. +3) into ring slot g % NG: wave w moves row w,
+    // 16-byte unit u = j*64 + lane of the row image from source offset doff[j]
+    uint32_t doff[ROW_INSTR];
+#pragma unroll
+    for (int j = 0; j < ROW_INSTR; ++j) {
+        const int u = j * 64 + lane;
+        const int p = u / (2 * HC), r = u - p * 2 * HC;
+        const int q = r >> 1, c = (r & 1) ^ ((q >> 3) & 1);
+        doff[j] = (uint32_t)((size_t)p * pstride + q * 32 + c * 16);
+    }
+    auto dma = [&](int g, int j) {
+        const int y = ys - 4 + GR * g + wave;  // within the buffer's zero border (pad 4)
+        glds16(xcol + (ptrdiff_t)y * xrow + doff[j], smem + OFF_IN + ((g % NG) * GR + wave) * ROWB + j * 1024);
+    };
+    // the B fragments of the 36 k-steps (chunk, kx, ks), resident for the whole strip
+    bf16x8 wr[36];
+#pragma unroll
+    for (int st = 0; st < 36; ++st) {
+        const int chunk = st / 18, kx = (st / 2) % 9, ks = st & 1, n = l31;
+        wr[st] = *reinterpret_cast<const bf16x8*>((const char*)d.wpack +
+                                                  ((((kx * 2 + chunk) * 2 + ks) * 32 + n) * 2 + (hh ^ ((n >> 3) & 1))) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < ROW_INSTR; ++j) dma(0, j);
+    if (nit > 1) {
+#pragma unroll
+        for (int j = 0; j < ROW_INSTR; ++j) dma(1, j);
+    }
+    unsigned long long t_entry = 0, t_wait = 0, t_loop = 0, t_a = 0;
+    if constexpr (ABL & 16) t_entry = rt_now();
+
+    const size_t plane = (size_t)d.h * d.w;
+    const int esz = d.y_u8 ? 1 : 4;
+    // unconditional buffer stores (lanes off the image get an offset past num_records and are
+    // dropped) so that every wave issues exactly ST stores per row
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)d.y + (size_t)img * 3 * plane * esz, (short)0, (int)(3 * plane * esz), 0x00020000);
+    // lanes 0..31 finish channels 0 and 1 of pixel l31, lanes 32..63 channel 2
+    const int cA = hh ? 2 : 0;
+    const float biasA = d.bias ? d.bias[cA] : 0.f, biasB = d.bias ? d.bias[1] : 0.f;
+    // O-ring slot of this lane's T column n = l31 = ky*3+co: row (T row - ky), position pos;
+    // n = 27..31 (padding columns of the MFMA) land in unread pad floats 29..33
+    const int wky = l31 < 27 ? l31 / 3 : 9;
+    const int wco = l31 - 3 * (l31 / 3);
+    const int wpos = l31 < 27 ? (wco == 0 ? wky : wco == 1 ? 9 + wky : 20 + wky) : 29 + (l31 - 27);
+    f32x16 accp;  // T row of the previous iteration, written into the O ring during this one
+
+    for (int i = 0; i <= nit + 1; ++i) {
+        const bool fin_prev2 = i - 2 >= 4, fin_prev1 = i - 1 >= 4;
+        // group i landed.  Younger VMEM ops that may stay in flight: the stores of iterations
+        // i-2 and i-1 and the DMA of group i+1
+        const int younger = ST * fin_prev2 + 5 * (i + 1 < nit) + ST * fin_prev1;
+        if constexpr (ABL & 16) t_a = rt_now();
+        if constexpr (ABL & 4) vm_wait(0); else vm_wait(younger);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // DMA of group i and the O writes of iteration i-1 visible
+        if constexpr (ABL & 16) {
+            const unsigned long long t = rt_now();
+            t_wait += t - t_a;
+            t_a = t;
+        }
+        const bool dma_on = !(ABL & 4) && i + 2 < nit;
+        const bool wprev = i >= 1 && i <= nit;  // O writes of T row 4(i-1)+w
+        float* wrow = T + ((GR * (i - 1) + wave - wky) & (NT - 1)) * (TW * TS) + 4 * hh * TS + wpos;
+        auto owrite = [&](int g) { wrow[((g & 3) + 8 * (g >> 2)) * TS] = accp[g]; };
+
+        // finish output row ys + r0 (O row r0 complete: T rows r0 .. r0+8 written by iteration i-1)
+        const bool fin = !(ABL & 2) && i >= 4;
+        const int r0 = GR * (i - 4) + wave;
+        f32x4 t4[5];  // lanes 0..31: O terms of channels 0 (t 0..8) and 1 (t 9..17); 32..63: channel 2 (t 0..8)
+        if (fin) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                t4[k] = lds_read16f4_async((const char*)(T + (r0 & (NT - 1)) * (TW * TS) + l31 * TS + 20 * hh + 4 * k));
+        }
+        const int yy = ys + r0, xx = x0 + l31;
+        const bool valid = yy < d.h && xx < d.w;
+        float sA = biasA, sB = biasB;
+        auto tv = [&](int n) { return t4[n >> 2][n & 3]; };
+        auto store = [&](float sv, int co, bool ok) {
+            const float t = tanhf(sv);
+            const int off = ok ? (int)((co * plane + (size_t)yy * d.w + xx) * esz) : 0x7ffffff0;
+            if (d.y_u8) {
+                const float q = rintf((t + 1.f) / 2.f * 255.f);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)fminf(fmaxf(q, 0.f), 255.f), yrs, off, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, t), yrs, off, 0, 0);
+            }
+        };
+
+        if (i < nit) {
+            // T row 4i + wave: the 1x9 row conv, k-steps in the per-tile kernels' order (chunk, kx, ks)
+            const char* row = smem + OFF_IN + ((i % NG) * GR + wave) * ROWB;
+            f32x16 acc;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+            bf16x8 fa[PD];
+            auto rd = [&](int st_, int slot) {
+                const int chunk = st_ / 18, kx = (st_ / 2) % 9, ks = st_ & 1;
+                fa[slot] = lds_read16_async(row + (chunk * 2 + ks) * (2 * HC) * 16 + halo_unit2(kx + l31, hh) * 16);
+            };
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s2 = 0; s2 < PD; ++s2) rd(s2, s2);
+#pragma unroll
+            for (int s2 = 0; s2 < 36; ++s2) {
+                // younger reads allowed in flight: those of steps s2+1 .. min(s2+PD-1, 35)
+                const int younger_rd = (35 - s2) < (PD - 1) ? (35 - s2) : (PD - 1);
+                if (s2 == 0) {
+                    lds_wait_t<PD - 1>(fa[0], t4);  // the older O-ring reads have landed as well
+                } else {
+                    switch (younger_rd) {
+                        case 5: lds_wait1<5>(fa[s2 % PD]); break;
+                        case 4: lds_wait1<4>(fa[s2 % PD]); break;
+                        case 3: lds_wait1<3>(fa[s2 % PD]); break;
+                        case 2: lds_wait1<2>(fa[s2 % PD]); break;
+                        case 1: lds_wait1<1>(fa[s2 % PD]); break;
+                        default: lds_wait1<0>(fa[s2 % PD]); break;
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (ABL & 1) {
+                    asm volatile("" ::"v"(fa[s2 % PD]), "v"(wr[s2]));
+                } else {
+                    acc = mfma32(fa[s2 % PD], wr[s2], acc);
+                }
+                if (s2 + PD < 36) rd(s2 + PD, s2 % PD);
+                // side jobs in this gap (see the schedule above)
+                if (s2 >= 1 && s2 <= ROW_INSTR && dma_on) dma(i + 2, s2 - 1);
+                if (s2 >= 6 && s2 < 22 && wprev) owrite(s2 - 6);
+                if (fin) {
+                    if (s2 >= 1 && s2 <= 9) {  // same order as the per-tile kernels: bias, ky 0..8
+                        sA += tv(s2 - 1);
+                        sB += tv(9 + s2 - 1);
+                    }
+                    if (s2 == 12) store(sA, cA, valid);
+                    if (s2 == 24) store(sB, 1, valid && hh == 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            accp = acc;
+        } else {
+            if (wprev) {
+#pragma unroll
+                for (int g = 0; g < 16; ++g) owrite(g);
+            }
+            if (fin) {
+                lds_wait_t4<0>(t4);
+#pragma unroll
+                for (int ky = 0; ky < 9; ++ky) {
+                    sA += tv(ky);
+                    sB += tv(9 + ky);
+                }
+                store(sA, cA, valid);
+                store(sB, 1, valid && hh == 0);
+            }
+        }
+        if constexpr (ABL & 16) t_loop += rt_now() - t_a;
+    }
+#ifdef ISR_TUNING
+    if constexpr (ABL & 16) {
+        unsigned long long* p = g_tail_stamps;
+        if (p != nullptr && lane == 0) {
+            unsigned long long* q = p + ((size_t)blockIdx.x * WM + wave) * 4;
+            q[0] = t_entry;
+            q[1] = rt_now();
+            q[2] = t_wait;
+            q[3] = t_loop;
+        }
+    }
+#endif
+}
+
 __global__ void pack_tail_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
     const int total = tail::W_BYTES / 2;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
@@ -640,6 +917,37 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             default: return go(tail9x9_pkernel<0>);
         }
     }
+    int abl = 0;
+#ifdef ISR_TUNING
+    if (variant >= 20 && variant < 52) {  // 20 + ABL: stream-tail ablations
+        abl = variant - 20;
+        variant = 4;
+    }
+#endif
+    if (variant == 4 && (size_t)3 * d->h * d->w * (d->y_u8 ? 1 : 4) >= ((size_t)1 << 31)) variant = 3;  // 32-bit store offsets
+    if (variant == 4) {
+        // segment height: 8 T rows per segment are recomputed by the neighbour (6 % at 128)
+        int sh = 128;
+        while (d->ha % sh) sh >>= 1;
+        if (sh < 8) return -2;
+        const int blocks = d->n * (d->wa / tails::TW) * (d->ha / sh);
+        auto go = [&](auto kern) {
+            lds_limit((const void*)kern, tails::LDS);
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), tails::LDS, s, *d, sh);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        };
+        switch (abl) {
+#ifdef ISR_TUNING
+            case 1: return go(tail9x9_stream_kernel<1>);
+            case 2: return go(tail9x9_stream_kernel<2>);
+            case 3: return go(tail9x9_stream_kernel<3>);
+            case 4: return go(tail9x9_stream_kernel<4>);
+            case 7: return go(tail9x9_stream_kernel<7>);
+            case 16: return go(tail9x9_stream_kernel<16>);
+#endif
+            default: return go(tail9x9_stream_kernel<0>);
+        }
+    }
     if (variant == 3) {
         lds_limit((const void*)tail9x9_k8_kernel, tail8::LDS);
         dim3 grid8(d->wa / tail8::TW, d->ha / tail8::TH, d->n);
@@ -652,6 +960,14 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
     hipLaunchKernelGGL(tail9x9_kernel, grid, dim3(256), tail::LDS, s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+#ifdef ISR_TUNING
+int tail_stamps_set(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tail_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#else
+int tail_stamps_set(void*) { return -2; }
+#endif
 
 int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s) { return tail9x9_fwd_variant(d, 0, s); }
 

@@ -29,6 +29,22 @@ __device__ __forceinline__ bf16x8 lds_read16(const char* p) {
     return *reinterpret_cast<const bf16x8*>(p);
 }
 
+// ds_read_b128 the compiler does not see as a load: the caller waits for it with its own
+// counted `s_waitcnt lgkmcnt(N)` (lds_wait).  For loops where hipcc's waitcnt insertion falls
+// back to lgkmcnt(0) before every MFMA.  Compiler-issued LDS ops around these only make the
+// counted waits stronger (lgkmcnt(N) retires all but the N youngest, whoever issued them).
+__device__ __forceinline__ bf16x8 lds_read16_async(const char* p) {
+    bf16x8 r;
+    const uint32_t a = (uint32_t)(uintptr_t)ISR_LDS_PTR(p);
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a) : "memory");
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(bf16x8& a, bf16x8& b) {
+    static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
+}
+
 // Asynchronous 16-byte-per-lane global → LDS copy (global_load_lds_dwordx4).
 // The LDS destination is wave-uniform `lds` + lane*16.
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds) {

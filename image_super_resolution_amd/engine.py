@@ -147,12 +147,15 @@ class GeneratorPlan:
     """
 
     def __init__(self, gw: GeneratorWeights, n: int, h: int, w: int, device, x_u8: bool, out_u8: bool,
-                 mean, std, variants: dict | None = None, chain: bool | None = None, chain_acquire: bool = False):
+                 mean, std, variants: dict | None = None, chain: bool | None = None,
+                 chain_acquire: bool | None = None):
         """`variants` (tuning only) maps ("conv3x3", cin, cout) or ("conv3x3", "*", cout)
         to an isr_conv3x3_fwd_variant id; unlisted convs use the production kernel.
         `chain` (default CHAIN_DEFAULT): the RRDB trunk as one persistent isr_conv_chain launch."""
         if chain is None:
             chain = CHAIN_DEFAULT
+        if chain_acquire is None:
+            chain_acquire = CHAIN_ACQUIRE
         self.key = (n, h, w, str(device), x_u8, out_u8, tuple(mean), tuple(std))
         bufs = GeneratorBuffers(n, h, w, len(gw.scalers), device)
         self.bufs = bufs
@@ -187,8 +190,12 @@ class GeneratorPlan:
         if chain and gw.rdb and not variants:
             # the whole RRDB trunk as ONE persistent launch (isr_conv_chain): tile-level
             # dependencies instead of 240 kernel boundaries
-            self.chain = ConvChain([d for _, d, _, _ in L[trunk0:]], X, device, acquire=chain_acquire)
-            L[trunk0:] = [(self.chain.fn, self.chain.desc, ("chain", len(L) - trunk0), None)]
+            try:
+                self.chain = ConvChain([d for _, d, _, _ in L[trunk0:]], X, device, acquire=chain_acquire)
+            except ValueError:  # e.g. buffers beyond the 2 GiB descriptor window: per-conv launches
+                self.chain = None
+            if self.chain is not None:
+                L[trunk0:] = [(self.chain.fn, self.chain.desc, ("chain", len(L) - trunk0), None)]
         c3(X, gw.conv1, feat, slope=1.0, r1=feat, s1=1.0)
         cur = feat
         for s, pc in enumerate(gw.scalers):
@@ -329,9 +336,11 @@ def _sleep_cycles_per_us() -> float:
 
 
 # The RRDB trunk runs as one persistent isr_conv_chain launch by default (ISR_CHAIN=0:
-# one launch per conv).
+# one launch per conv); ISR_CHAIN_ACQUIRE=0 drops the per-tile agent-scope acquire and
+# relies on the sc1 (L1-bypassing) activation loads alone (-1.5 % time).
 import os as _os
-CHAIN_DEFAULT = _os.environ.get("ISR_CHAIN", "0") == "1"
+CHAIN_DEFAULT = _os.environ.get("ISR_CHAIN", "1") == "1"
+CHAIN_ACQUIRE = _os.environ.get("ISR_CHAIN_ACQUIRE", "1") == "1"
 
 # Batches of >= 2 (even) are split over this many HIP streams by default: two
 # half-batch launch lists run concurrently, so one stream's kernel tail, prologue

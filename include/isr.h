@@ -315,6 +315,10 @@ int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_
  * done, epilogue done [s_memrealtime, 100 MHz], -, -, HW_ID, XCC_ID); NULL stops.
  * A default build returns ISR_ERR_UNSUPPORTED. */
 int isr_tuning_conv_stamps(void* buf);
+/* Tuning builds only: per-wave stamps of later row-streaming tail launches (tail variant
+ * 36 = 4 with stamps) into `buf` (4 x uint64 per (block, wave): entry, exit, summed
+ * top-of-row-group wait + barrier, summed loop; s_memrealtime ticks); NULL stops. */
+int isr_tuning_tail_stamps(void* buf);
 /* Validation only: ISR_OK when isr_conv3x3_fwd would accept `d` (nothing launched). */
 int isr_conv3x3_check(const isr_conv_desc* d);
 

@@ -5,7 +5,7 @@
 #   profiles/<R>_pmc_traffic.json         HBM bytes per launch of the dominant kernel (read by bench.py)
 #   profiles/<R>_bench.json               the bench line after the traffic file exists
 #   profiles/<R>_train_kernel_stats.csv   rocprofv3 --kernel-trace --stats of tools/bench_train.py (cfg3 step)
-# usage: tools/make_profiles.sh r01
+# usage: tools/make_profiles.sh r02
 set -eu
 R=${1:-r01}
 export TMPDIR=/tmp
@@ -15,19 +15,16 @@ mkdir -p $P $T
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/prof_bench -o bench -- \
   python3 bench.py --round $R > $P/prof_bench.json 2> $T/prof_bench.err
 cp $T/prof_bench/bench_kernel_stats.csv $P/${R}_bench_kernel_stats.csv
-# the dominant kernel per grid: bench.py runs it at two grids (half batch inside the
-# 2-stream timed forwards, full batch in the isolated single-stream roofline timing);
-# --stats averages both, the roofline compares against the full-batch row
+# the dominant kernel (the persistent trunk kernel): its launches from the trace
 python3 - "$T/prof_bench/bench_kernel_trace.csv" "$P/${R}_bench_dominant_by_grid.json" <<'EOF2'
 import csv, json, sys
 from collections import defaultdict
-rows = [r for r in csv.DictReader(open(sys.argv[1]))
-        if "conv3x3_fwd_kernel" in r["Kernel_Name"] and ", 192, " in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_chain_kernel" in r["Kernel_Name"]]
 by = defaultdict(list)
 for r in rows:
     by[int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 out = [{"kernel": rows[0]["Kernel_Name"], "blocks": b, "dispatches": len(v), "avg_us": round(sum(v) / len(v) / 1e3, 3),
-        "role": "full batch, single stream (bench roofline)" if b == max(by) else "half batch, 2 concurrent streams (timed forwards)"}
+        "role": "persistent trunk kernel, one launch per forward"}
        for b, v in sorted(by.items())]
 json.dump(out, open(sys.argv[2], "w"), indent=1)
 print(json.dumps(out))
@@ -38,17 +35,27 @@ python3 - "$R" "$P" <<'EOF'
 import json, sys
 R, P = sys.argv[1], sys.argv[2]
 rows = json.load(open(f"{P}/{R}_pmc_summary.json"))
-dom = [r for r in rows if "conv3x3_fwd_kernel" in r["kernel"] and ", 192, " in r["kernel"]]  # RDB final conv (V_F0)
-if dom:
-    r = max(dom, key=lambda r: int(r["grid"]))  # the full-batch grid (bench.py's roofline launches)
-    out = {"kernel": r["kernel"], "grid": r["grid"], "dispatches": r["dispatches"],
-           "hbm_bytes_per_launch": r["hbm_bytes"], "hbm_read_bytes": r["hbm_read_bytes"],
-           "hbm_write_bytes": r["hbm_write_bytes"],
-           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, KiB -> bytes, FETCH_SIZE x2 "
-                     "(gfx950 wide-load correction, MI355X_MICROARCH.md §HBM); mean over dispatches; "
-                     "Infinity-Cache hits are included in these counters"}
-    json.dump(out, open(f"{P}/{R}_pmc_traffic.json", "w"), indent=1)
-    print("traffic", out["hbm_bytes_per_launch"])
+# kernel families bench.py reports a roofline for (bench.py load_traffic): the persistent
+# trunk kernel, the per-conv growth (V_G0) and final (V_F0) templates, the 9x9 tail
+fam = {"chain": "conv_chain_kernel", "growth": "C3<4, 4, 1, 16, 2, 0, 0, 2",
+       "final": "C3<4, 4, 2, 16, 2, 192", "tail": "tail9x9_"}
+out = {"families": {},
+       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, KiB -> bytes, FETCH_SIZE x2 "
+                 "(gfx950 wide-load correction, MI355X_MICROARCH.md §HBM); mean over dispatches of the "
+                 "largest grid of the family; Infinity-Cache hits are included in these counters"}
+for k, sub in fam.items():
+    dom = [r for r in rows if sub in r["kernel"] and (k != "growth" or "conv_chain" not in r["kernel"])]
+    if not dom:
+        continue
+    g = max(int(r["grid"]) for r in dom)
+    sel = [r for r in dom if int(r["grid"]) == g]
+    nd = sum(r["dispatches"] for r in sel)
+    avg = lambda key: sum(r[key] * r["dispatches"] for r in sel) / nd
+    out["families"][k] = {"kernel": sel[0]["kernel"], "grid": g, "dispatches": nd,
+                          "hbm_bytes_per_launch": avg("hbm_bytes"), "hbm_read_bytes": avg("hbm_read_bytes"),
+                          "hbm_write_bytes": avg("hbm_write_bytes")}
+    print("traffic", k, out["families"][k]["hbm_bytes_per_launch"])
+json.dump(out, open(f"{P}/{R}_pmc_traffic.json", "w"), indent=1)
 EOF
 cp $P/${R}_pmc_traffic.json profiles/ 2>/dev/null || true
 timeout -k 10 600 python3 bench.py --round $R > $P/${R}_bench.json 2> $T/bench_final.err
