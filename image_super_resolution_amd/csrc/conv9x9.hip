@@ -676,7 +676,7 @@ __device__ __forceinline__ unsigned long long rt_now() {
 //   gaps 1..9    ky sums of output row 4(i-4)+w (its O-ring terms read before the prefetch)
 //   gaps 12, 24  tanh + store of its two channel slots
 // so a T row is written one iteration after it is computed and read one iteration later.
-template <int ABL>
+template <int ABL, int PD = tails::PD>
 __global__ __launch_bounds__(256, 1) void tail9x9_stream_kernel(isr_tail_desc d, int sh) {
     using namespace tails;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -757,6 +757,12 @@ __global__ __launch_bounds__(256, 1) void tail9x9_stream_kernel(isr_tail_desc d,
             t_a = t;
         }
         const bool dma_on = !(ABL & 4) && i + 2 < nit;
+        if constexpr (ABL & 64) {  // tuning: the group's DMA right after the barrier instead of in gaps 1..5
+            if (dma_on) {
+#pragma unroll
+                for (int j = 0; j < ROW_INSTR; ++j) dma(i + 2, j);
+            }
+        }
         const bool wprev = i >= 1 && i <= nit;  // O writes of T row 4(i-1)+w
         float* wrow = T + ((GR * (i - 1) + wave - wky) & (NT - 1)) * (TW * TS) + 4 * hh * TS + wpos;
         auto owrite = [&](int g) { wrow[((g & 3) + 8 * (g >> 2)) * TS] = accp[g]; };
@@ -807,6 +813,12 @@ __global__ __launch_bounds__(256, 1) void tail9x9_stream_kernel(isr_tail_desc d,
                     lds_wait_t<PD - 1>(fa[0], t4);  // the older O-ring reads have landed as well
                 } else {
                     switch (younger_rd) {
+                        case 11: lds_wait1<11>(fa[s2 % PD]); break;
+                        case 10: lds_wait1<10>(fa[s2 % PD]); break;
+                        case 9: lds_wait1<9>(fa[s2 % PD]); break;
+                        case 8: lds_wait1<8>(fa[s2 % PD]); break;
+                        case 7: lds_wait1<7>(fa[s2 % PD]); break;
+                        case 6: lds_wait1<6>(fa[s2 % PD]); break;
                         case 5: lds_wait1<5>(fa[s2 % PD]); break;
                         case 4: lds_wait1<4>(fa[s2 % PD]); break;
                         case 3: lds_wait1<3>(fa[s2 % PD]); break;
@@ -823,7 +835,7 @@ __global__ __launch_bounds__(256, 1) void tail9x9_stream_kernel(isr_tail_desc d,
                 }
                 if (s2 + PD < 36) rd(s2 + PD, s2 % PD);
                 // side jobs in this gap (see the schedule above)
-                if (s2 >= 1 && s2 <= ROW_INSTR && dma_on) dma(i + 2, s2 - 1);
+                if (!(ABL & 64) && s2 >= 1 && s2 <= ROW_INSTR && dma_on) dma(i + 2, s2 - 1);
                 if (s2 >= 6 && s2 < 22 && wprev) owrite(s2 - 6);
                 if (fin) {
                     if (s2 >= 1 && s2 <= 9) {  // same order as the per-tile kernels: bias, ky 0..8
@@ -868,6 +880,363 @@ __global__ __launch_bounds__(256, 1) void tail9x9_stream_kernel(isr_tail_desc d,
 #endif
 }
 
+// ---- row-streaming tail, 8 waves (variant 5): the variant-4 walk with two waves per SIMD.
+// One wave per SIMD left every non-MFMA cost of the wave (LDS-DMA issue, the finish's VALU,
+// LDS waits) on the MFMA chain's critical path; with a partner wave those stalls overlap the
+// partner's MFMAs.  Eight T rows per iteration (one per wave), input rows double-buffered
+// (group i+1's DMA issued in the gaps of iteration i), the O ring (keyed by output row, as in
+// variant 4) written at the end of the iteration; after barrier #2 the next iteration reads its
+// O terms into registers before its top barrier, so O row r0 lives two iterations: 16 rows.
+// Bit-identical to variants 1/3/4 (same MFMA order per T element, same ky-sum order).
+namespace tail8w {
+constexpr int TW = 32, WM = 8, GR = 8;       // strip width, waves, rows per group (one per wave)
+constexpr int HC = TW + 8;
+constexpr int ROWB = 4 * HC * 32;             // 5120
+constexpr int ROW_INSTR = ROWB / 1024;        // 5
+constexpr int NG = 2;
+constexpr int NT = 16;
+constexpr int TS = tails::TS;                 // O row as in variant 4: [px][co 0: 0..8, co 1: 9..17, co 2: 20..28]
+constexpr int TROW = TW * TS * 4;             // 4608
+constexpr int OFF_IN = 0;
+constexpr int OFF_T = OFF_IN + NG * GR * ROWB;      // 81920
+constexpr int LDS = OFF_T + NT * TROW + 64;        // 155712 (+64: lanes 32..63 of px 31 read 4 floats past a row)
+constexpr int PD = 4;
+constexpr int ST = 2;
+static_assert(LDS <= 163840, "LDS");
+}  // namespace tail8w
+
+template <int ABL, int PD = tail8w::PD>
+__global__ __launch_bounds__(512, 1) void tail9x9_stream8_kernel(isr_tail_desc d, int sh) {
+    using namespace tail8w;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nstrip = d.wa / TW, nseg = d.ha / sh;
+    int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int strip = b % nstrip;
+    b /= nstrip;
+    const int seg = b % nseg;
+    const int img = b / nseg;
+    const int x0 = strip * TW, ys = seg * sh;
+    const int wave = wave_id();
+    const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+    const int nit = sh / GR + 1;  // T rows ys-4 .. ys+sh+3, eight per iteration
+    float* T = reinterpret_cast<float*>(smem + OFF_T);
+    const size_t pstride = plane_bytes(d.x);
+    const char* xcol = view_at(d.x, img, 0, x0 - 4, 0);
+    const int xrow = d.x.wp * 32;
+
+    uint32_t doff[ROW_INSTR];
+#pragma unroll
+    for (int j = 0; j < ROW_INSTR; ++j) {
+        const int u = j * 64 + lane;
+        const int p = u / (2 * HC), r = u - p * 2 * HC;
+        const int q = r >> 1, c = (r & 1) ^ ((q >> 3) & 1);
+        doff[j] = (uint32_t)((size_t)p * pstride + q * 32 + c * 16);
+    }
+    auto dma = [&](int g, int j) {
+        const int y = ys - 4 + GR * g + wave;  // within the buffer's zero border (pad 4)
+        glds16(xcol + (ptrdiff_t)y * xrow + doff[j], smem + OFF_IN + ((g % NG) * GR + wave) * ROWB + j * 1024);
+    };
+    bf16x8 wr[36];
+#pragma unroll
+    for (int st = 0; st < 36; ++st) {
+        const int chunk = st / 18, kx = (st / 2) % 9, ks = st & 1, n = l31;
+        wr[st] = *reinterpret_cast<const bf16x8*>((const char*)d.wpack +
+                                                  ((((kx * 2 + chunk) * 2 + ks) * 32 + n) * 2 + (hh ^ ((n >> 3) & 1))) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < ROW_INSTR; ++j) dma(0, j);
+
+    const size_t plane = (size_t)d.h * d.w;
+    const int esz = d.y_u8 ? 1 : 4;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)d.y + (size_t)img * 3 * plane * esz, (short)0, (int)(3 * plane * esz), 0x00020000);
+    const int cA = hh ? 2 : 0;
+    const float biasA = d.bias ? d.bias[cA] : 0.f, biasB = d.bias ? d.bias[1] : 0.f;
+    const int wky = l31 < 27 ? l31 / 3 : 9;
+    const int wco = l31 - 3 * (l31 / 3);
+    const int wpos = l31 < 27 ? (wco == 0 ? wky : wco == 1 ? 9 + wky : 20 + wky) : 29 + (l31 - 27);
+    uint32_t aoff[9];
+#pragma unroll
+    for (int kx = 0; kx < 9; ++kx) aoff[kx] = halo_unit2(kx + l31, hh) * 16;
+
+    f32x4 t4[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t4[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto tv = [&](int n) { return t4[n >> 2][n & 3]; };
+
+    for (int i = 0; i <= nit; ++i) {
+        const bool fin = !(ABL & 2) && i >= 2;
+        // this iteration's O terms (output row ys + 8(i-2) + wave): the O ring is complete up to
+        // it since barrier #2 of the previous iteration.  Issued here, at the top, so no asm
+        // load is in flight across the loop's back-edge (the compiler may copy such registers)
+        const int r0 = GR * (i - 2) + wave;
+        if (fin) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                t4[k] = lds_read16f4_async((const char*)(T + (r0 & (NT - 1)) * (TW * TS) + l31 * TS + 20 * hh + 4 * k));
+        }
+        // own row of group i landed; younger VMEM: the stores of iteration i-1
+        const int younger = ST * (!(ABL & 2) && i - 1 >= 2);
+        if (ABL & 4) vm_wait(0); else vm_wait(younger);
+        lds_wait_t4<0>(t4);
+        // top barrier: LDS-DMA data (vmcnt, then a barrier, then ds_read), and every wave holds
+        // its O terms, so their ring slots may be rewritten by this iteration's T writes
+        __builtin_amdgcn_s_barrier();
+        const bool dma_on = !(ABL & 4) && i + 1 < nit;
+        const int yy = ys + r0, xx = x0 + l31;
+        const bool valid = yy < d.h && xx < d.w;
+        float sA = biasA, sB = biasB;
+        auto store = [&](float sv, int co, bool ok) {
+            const float t = tanhf(sv);
+            const int off = ok ? (int)((co * plane + (size_t)yy * d.w + xx) * esz) : 0x7ffffff0;
+            if (d.y_u8) {
+                const float q = rintf((t + 1.f) / 2.f * 255.f);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)fminf(fmaxf(q, 0.f), 255.f), yrs, off, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, t), yrs, off, 0, 0);
+            }
+        };
+
+        if (i < nit) {
+            const char* row = smem + OFF_IN + ((i % NG) * GR + wave) * ROWB;
+            f32x16 acc;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+            bf16x8 fa[PD];
+            auto rd = [&](int st_, int slot) {
+                const int chunk = st_ / 18, kx = (st_ / 2) % 9, ks = st_ & 1;
+                fa[slot] = lds_read16_async(row + (chunk * 2 + ks) * (2 * HC) * 16 + aoff[kx]);
+            };
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s2 = 0; s2 < PD; ++s2) rd(s2, s2);
+#pragma unroll
+            for (int s2 = 0; s2 < 36; ++s2) {
+                const int younger_rd = (35 - s2) < (PD - 1) ? (35 - s2) : (PD - 1);
+                switch (younger_rd) {
+                    case 5: lds_wait1<5>(fa[s2 % PD]); break;
+                    case 4: lds_wait1<4>(fa[s2 % PD]); break;
+                    case 3: lds_wait1<3>(fa[s2 % PD]); break;
+                    case 2: lds_wait1<2>(fa[s2 % PD]); break;
+                    case 1: lds_wait1<1>(fa[s2 % PD]); break;
+                    default: lds_wait1<0>(fa[s2 % PD]); break;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (ABL & 1) {
+                    asm volatile("" ::"v"(fa[s2 % PD]), "v"(wr[s2]));
+                } else {
+                    acc = mfma32(fa[s2 % PD], wr[s2], acc);
+                }
+                if (s2 + PD < 36) rd(s2 + PD, s2 % PD);
+                if (s2 >= 1 && s2 <= ROW_INSTR && dma_on) dma(i + 1, s2 - 1);
+                if (fin) {
+                    if (s2 >= 1 && s2 <= 9) {  // same order as the per-tile kernels: bias, ky 0..8
+                        sA += tv(s2 - 1);
+                        sB += tv(9 + s2 - 1);
+                    }
+                    if (s2 == 12) store(sA, cA, valid);
+                    if (s2 == 24) store(sB, 1, valid && hh == 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // T row 8i + wave into the O ring: T(r, px, n = ky*3+co) -> O[r - ky][px][pos(co, ky)]
+            float* wrow = T + ((GR * i + wave - wky) & (NT - 1)) * (TW * TS) + 4 * hh * TS + wpos;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) wrow[((g & 3) + 8 * (g >> 2)) * TS] = acc[g];
+        } else if (fin) {
+#pragma unroll
+            for (int ky = 0; ky < 9; ++ky) {
+                sA += tv(ky);
+                sB += tv(9 + ky);
+            }
+            store(sA, cA, valid);
+            store(sB, 1, valid && hh == 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // barrier #2: every T row of iteration i is in the O ring
+    }
+}
+
+// ---- lane-streaming tail (variant 6): one WAVE walks one 32-column strip down `sh` output rows,
+// with no barriers and no cross-wave state.  Per input row: the 36-MFMA chain gives T[px][n'] with
+// the weight columns permuted to n' = co*9 + ky + 1, so the nine ky terms of one channel sit in
+// nine adjacent lanes; a running partial sum P (16 px per lane) then advances ONE lane per row:
+// P[n'] <- P[n'-1] (v_add_f32 with DPP wave_shr:1) + T[n'].  Output row y's channel-co sum is
+// bias (injected at lane 9co) + T(y-4)[ky 0] + ... + T(y+4)[ky 8], added in exactly that order —
+// the per-tile kernels' order — and complete in lane 9co+9 one row after its last term: written
+// to a small per-wave LDS buffer, then tanh'ed and stored two output rows at a time with all 64
+// lanes busy.  Input rows stream through a per-wave 3-row LDS ring (LDS-DMA two rows ahead,
+// waited by counted vmcnt: same wave, no barrier).  Bit-identical to variants 1/3/4/5.
+namespace tailw {
+constexpr int TW = 32, WPB = 4;               // strip width, waves per block (independent)
+constexpr int HC = TW + 8;
+constexpr int ROWB = 4 * HC * 32;             // 5120: one input row image
+constexpr int ROW_INSTR = ROWB / 1024;        // 5
+constexpr int NR = 3;                         // rows in a wave's ring
+constexpr int FB = 2 * 2 * 3 * TW * 4;        // finished-sum buffer: [slot 2][row 2][co 3][px 32] fp32 = 1536
+constexpr int WAVE_LDS = NR * ROWB + FB;      // 16896
+constexpr int LDS = WPB * WAVE_LDS;           // 67584: two blocks per CU
+constexpr int PD = 2;
+constexpr int FLUSH_ST = 3;                   // stores per flush (2 rows x 3 co x 32 px over 64 lanes)
+static_assert(2 * LDS <= 163840, "two blocks per CU");
+}  // namespace tailw
+
+__device__ __forceinline__ float dpp_shr1(float v) {  // lane i <- lane i-1 (lane 0 <- 0)
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+
+template <int ABL, int MINB = 2>
+__global__ __launch_bounds__(256, MINB) void tail9x9_lane_kernel(isr_tail_desc d, int sh, int nwaves) {
+    using namespace tailw;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int wave = wave_id();
+    const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+    const int nstrip = d.wa / TW, nseg = d.ha / sh;
+    int gw = xcd_remap(blockIdx.x, gridDim.x) * WPB + wave;  // neighbouring strips in one block / XCD
+    if (gw >= nwaves) return;  // whole wave (no barriers in this kernel)
+    const int strip = gw % nstrip;
+    gw /= nstrip;
+    const int seg = gw % nseg;
+    const int img = gw / nseg;
+    const int x0 = strip * TW, ys = seg * sh;
+    const int nt = sh + 8;  // T rows ys-4 .. ys+sh+3
+    char* ring = smem + wave * WAVE_LDS;
+    float* fbuf = reinterpret_cast<float*>(ring + NR * ROWB);
+    const size_t pstride = plane_bytes(d.x);
+    const char* xcol = view_at(d.x, img, 0, x0 - 4, 0);
+    const int xrow = d.x.wp * 32;
+
+    auto dma = [&](int t, int j) {  // input row of T row t (= image row ys-4+t) into ring slot t % NR
+        const int u = j * 64 + lane;  // 16-byte unit of the row image
+        const int p = u / (2 * HC), r = u - p * 2 * HC;
+        const int q = r >> 1, c = (r & 1) ^ ((q >> 3) & 1);
+        glds16(xcol + (ptrdiff_t)(ys - 4 + t) * xrow + (size_t)p * pstride + q * 32 + c * 16,
+               ring + (t % NR) * ROWB + j * 1024);
+    };
+    // B fragments with the permuted columns: lane column n' = co*9 + ky + 1 takes packed n = ky*3 + co
+    const int np = l31 - 1;
+    const bool wcol = np >= 0 && np < 27;
+    const int wco = wcol ? np / 9 : 0, wky = wcol ? np - 9 * (np / 9) : 0;
+    const int pn = wky * 3 + wco;
+    bf16x8 wr[36];
+#pragma unroll
+    for (int st = 0; st < 36; ++st) {
+        const int chunk = st / 18, kx = (st / 2) % 9, ks = st & 1;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+            (const char*)d.wpack + ((((kx * 2 + chunk) * 2 + ks) * 32 + pn) * 2 + (hh ^ ((pn >> 3) & 1))) * 16);
+        wr[st] = wcol ? v : bf16x8{};
+    }
+#pragma unroll
+    for (int j = 0; j < ROW_INSTR; ++j) dma(0, j);
+#pragma unroll
+    for (int j = 0; j < ROW_INSTR; ++j) dma(1, j);
+
+    // bias injection: lane 9co (co = 0, 1, 2) holds bias[co] before the shift, which lane 9co+1 reads
+    const bool inj = l31 == 0 || l31 == 9 || l31 == 18;
+    const float binj = d.bias ? d.bias[l31 == 0 ? 0 : l31 == 9 ? 1 : 2] : 0.f;
+    const bool done_lane = l31 == 9 || l31 == 18 || l31 == 27;  // ky = 8 of channel (l31 - 9) / 9
+    const int dco = l31 / 9 - 1;
+
+    const size_t plane = (size_t)d.h * d.w;
+    const int esz = d.y_u8 ? 1 : 4;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)d.y + (size_t)img * 3 * plane * esz, (short)0, (int)(3 * plane * esz), 0x00020000);
+
+    f32x16 P;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) P[g] = 0.f;
+    // flush of the finished pair in slot fs (output rows ys + 2*pr, +1): 3 values per lane
+    float fv[3];
+    int fpr = 0;
+    auto flush_read = [&](int fs) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) fv[j] = fbuf[fs * 192 + j * 64 + lane];
+    };
+    auto flush_store = [&](int j) {  // element k = j*64 + lane of [row 2][co 3][px 32]
+        const int k = j * 64 + lane;
+        const int rr = k / 96, co = (k / 32) % 3, px = k & 31;
+        const int yy = ys + 2 * fpr + rr, xx = x0 + px;
+        const float t = tanhf(fv[j]);
+        const int off = (yy < d.h && xx < d.w) ? (int)((co * plane + (size_t)yy * d.w + xx) * esz) : 0x7ffffff0;
+        if (d.y_u8) {
+            const float q = rintf((t + 1.f) / 2.f * 255.f);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)fminf(fmaxf(q, 0.f), 255.f), yrs, off, 0, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, t), yrs, off, 0, 0);
+        }
+    };
+
+    for (int t = 0; t < nt; ++t) {
+        // row t landed.  Younger VMEM ops possibly in flight: the flush stores of rows t-2 and
+        // t-1 (a flush runs in even rows >= 10) and the DMA of row t+1
+        auto flushes = [&](int u) { return u >= 10 && (u & 1) == 0 && !(ABL & 2); };
+        const int younger = FLUSH_ST * flushes(t - 2) + ROW_INSTR * (t + 1 < nt) + FLUSH_ST * flushes(t - 1);
+        if (ABL & 4) vm_wait(0); else vm_wait(younger);
+        const bool dma_on = !(ABL & 4) && t + 2 < nt;
+        const bool fl = flushes(t);
+        if (fl) fpr = (t - 10) / 2;  // output pair (rows ys + 2*fpr, +1) finished in rows t-2, t-1
+
+        const char* row = ring + (t % NR) * ROWB;
+        f32x16 acc;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+        bf16x8 fa[PD];
+        auto rd = [&](int st_, int slot) {
+            const int chunk = st_ / 18, kx = (st_ / 2) % 9, ks = st_ & 1;
+            fa[slot] = lds_read16_async(row + (chunk * 2 + ks) * (2 * HC) * 16 + halo_unit2(kx + l31, hh) * 16);
+        };
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s2 = 0; s2 < PD; ++s2) rd(s2, s2);
+#pragma unroll
+        for (int s2 = 0; s2 < 36; ++s2) {
+            const int younger_rd = (35 - s2) < (PD - 1) ? (35 - s2) : (PD - 1);
+            switch (younger_rd) {
+                case 3: lds_wait1<3>(fa[s2 % PD]); break;
+                case 2: lds_wait1<2>(fa[s2 % PD]); break;
+                case 1: lds_wait1<1>(fa[s2 % PD]); break;
+                default: lds_wait1<0>(fa[s2 % PD]); break;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ABL & 1) {
+                asm volatile("" ::"v"(fa[s2 % PD]), "v"(wr[s2]));
+            } else {
+                acc = mfma32(fa[s2 % PD], wr[s2], acc);
+            }
+            if (s2 + PD < 36) rd(s2 + PD, s2 % PD);
+            if (s2 >= 1 && s2 <= ROW_INSTR && dma_on) dma(t + 2, s2 - 1);
+            if (fl) {
+                if (s2 == 6) flush_read(((t - 10) / 2) & 1);
+                if (s2 == 12) flush_store(0);
+                if (s2 == 20) flush_store(1);
+                if (s2 == 28) flush_store(2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // running sums: inject the biases, shift one lane, add this row's terms
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const float pin = inj ? binj : P[g];
+            P[g] = dpp_shr1(pin) + acc[g];
+        }
+        // lanes 9/18/27 now hold output row ys + t - 8 of channel dco: to the flush buffer
+        if (t >= 8 && done_lane) {
+            const int u = t - 8;  // output row index in the segment
+            float* fr = fbuf + ((u >> 1) & 1) * 192 + (u & 1) * 96 + dco * 32 + 4 * hh;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) fr[(g & 3) + 8 * (g >> 2)] = P[g];
+        }
+    }
+    // the last pair (rows sh-2, sh-1), finished in rows nt-2, nt-1
+    if (!(ABL & 2)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        fpr = (sh - 2) / 2;
+        flush_read(fpr & 1);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) flush_store(j);
+    }
+}
+
 __global__ void pack_tail_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
     const int total = tail::W_BYTES / 2;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
@@ -896,10 +1265,11 @@ int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s) {
 }
 
 int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
-    // production = variant 3, the 8-row tile with two blocks per CU (381 vs 401 us for the
-    // 16-row one-block-per-CU variant 1 at 16 x 512², bit-identical outputs); the persistent
-    // variant 2 measures 515 us (LDS-atomic slices: 990 us; tools/tune_tail.py)
-    if (variant == 0) variant = 3;
+    // production = variant 5, the 8-wave row-streaming walk: 170-177 us at 16 x 512² (fp32
+    // out) vs 354-375 us for the 8-row per-tile kernel (variant 3), 259-280 us for the 4-wave
+    // walk (4) and 236-280 us for the lane-streaming walk (6), all bit-identical
+    // (tools/tune_tail.py, tests/test_gpu_kernels.py); the persistent variant 2 measures 515 us
+    if (variant == 0) variant = 5;
     if (variant == 2 || (variant >= 10 && variant <= 17)) {  // persistent
         const int cus = cu_count();
         const int ntiles = d->n * (d->ha / tail::TH) * (d->wa / tail::TW);
@@ -917,14 +1287,80 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             default: return go(tail9x9_pkernel<0>);
         }
     }
-    int abl = 0;
+    int abl = 0, lane_sh = 0;
 #ifdef ISR_TUNING
-    if (variant >= 20 && variant < 52) {  // 20 + ABL: stream-tail ablations
+    if (variant >= 20 && variant < 70) {  // 20 + ABL: stream-tail ablations
         abl = variant - 20;
         variant = 4;
+    } else if (variant >= 70 && variant < 78) {  // 70 + ABL: 8-wave stream-tail ablations
+        abl = variant - 70;
+        variant = 5;
+    } else if (variant >= 80 && variant < 88) {  // 80 + ABL: lane-streaming ablations
+        abl = variant - 80;
+        variant = 6;
+    } else if (variant >= 90 && variant < 98) {  // 90 + log2(sh): lane-streaming segment height
+        lane_sh = 1 << (variant - 90);
+        variant = 6;
+    } else if (variant >= 100 && variant < 108) {  // 100 + log2(sh): one wave per SIMD
+        lane_sh = 1 << (variant - 100);
+        abl = 8;
+        variant = 6;
+    } else if (variant >= 110 && variant < 118) {  // the same without row DMA
+        lane_sh = 1 << (variant - 110);
+        abl = 9;
+        variant = 6;
     }
 #endif
-    if (variant == 4 && (size_t)3 * d->h * d->w * (d->y_u8 ? 1 : 4) >= ((size_t)1 << 31)) variant = 3;  // 32-bit store offsets
+    if ((variant == 4 || variant == 5 || variant == 6) && (size_t)3 * d->h * d->w * (d->y_u8 ? 1 : 4) >= ((size_t)1 << 31)) variant = 3;  // 32-bit store offsets
+    if (variant == 6) {
+        int sh = lane_sh;
+        if (sh == 0) {
+            sh = 64;
+            while (d->ha % sh) sh >>= 1;
+        }
+        if (sh < 8 || d->ha % sh) return -2;
+        const int nwaves = d->n * (d->wa / tailw::TW) * (d->ha / sh);
+        const int blocks = (nwaves + tailw::WPB - 1) / tailw::WPB;
+        auto go = [&](auto kern) {
+            lds_limit((const void*)kern, tailw::LDS);
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), tailw::LDS, s, *d, sh, nwaves);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        };
+        switch (abl) {
+#ifdef ISR_TUNING
+            case 1: return go(tail9x9_lane_kernel<1>);
+            case 2: return go(tail9x9_lane_kernel<2>);
+            case 4: return go(tail9x9_lane_kernel<4>);
+            case 7: return go(tail9x9_lane_kernel<7>);
+            case 8: return go(tail9x9_lane_kernel<0, 1>);  // one wave per SIMD (no register cap)
+            case 9: return go(tail9x9_lane_kernel<4, 1>);
+#endif
+            default: return go(tail9x9_lane_kernel<0>);
+        }
+    }
+    if (variant == 5) {
+        int sh = 128;
+        while (d->ha % sh) sh >>= 1;
+        if (sh < 8) return -2;
+        const int blocks = d->n * (d->wa / tail8w::TW) * (d->ha / sh);
+        auto go = [&](auto kern) {
+            lds_limit((const void*)kern, tail8w::LDS);
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(512), tail8w::LDS, s, *d, sh);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        };
+        switch (abl) {
+#ifdef ISR_TUNING
+            case 1: return go(tail9x9_stream8_kernel<1>);
+            case 2: return go(tail9x9_stream8_kernel<2>);
+            case 4: return go(tail9x9_stream8_kernel<4>);
+            case 7: return go(tail9x9_stream8_kernel<7>);
+            case 3: return go(tail9x9_stream8_kernel<0, 3>);
+            case 5: return go(tail9x9_stream8_kernel<0, 5>);
+            case 6: return go(tail9x9_stream8_kernel<0, 6>);
+#endif
+            default: return go(tail9x9_stream8_kernel<0>);
+        }
+    }
     if (variant == 4) {
         // segment height: 8 T rows per segment are recomputed by the neighbour (6 % at 128)
         int sh = 128;
@@ -942,8 +1378,15 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             case 2: return go(tail9x9_stream_kernel<2>);
             case 3: return go(tail9x9_stream_kernel<3>);
             case 4: return go(tail9x9_stream_kernel<4>);
+            case 5: return go(tail9x9_stream_kernel<5>);
+            case 6: return go(tail9x9_stream_kernel<6>);
             case 7: return go(tail9x9_stream_kernel<7>);
             case 16: return go(tail9x9_stream_kernel<16>);
+            case 49: return go(tail9x9_stream_kernel<64>);  // variant 69: DMA right after the barrier
+            case 32 + 4: return go(tail9x9_stream_kernel<0, 4>);  // 20 + 32 + PD: prefetch distance
+            case 32 + 8: return go(tail9x9_stream_kernel<0, 8>);
+            case 32 + 10: return go(tail9x9_stream_kernel<0, 10>);
+            case 32 + 12: return go(tail9x9_stream_kernel<0, 12>);
 #endif
             default: return go(tail9x9_stream_kernel<0>);
         }

@@ -347,8 +347,11 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
 
 int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s);
 int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);
-/* Tuning / A-B entry point: 0 = production (= 3), 1 = one tile per block, 3 = one 8-row tile per block (76 KB LDS, 2 blocks / CU), 2 = persistent
- * (one block per CU, streamed halo ring; slower: its partial-sum epilogue dominates).
+/* Tuning / A-B entry point: 0 = production (= 5), 1 = one 16-row tile per block, 3 = one
+ * 8-row tile per block (76 KB LDS, 2 blocks / CU), 2 = persistent (one block per CU, streamed
+ * halo ring), 4 = row-streaming walk down a 32-column strip (4 waves, each T row computed
+ * once), 5 = the same walk with 8 waves (two per SIMD), 6 = lane-streaming walk (one wave per
+ * strip, running ky sums shifted one lane per row).  All bit-identical.
  * Same descriptor rules as isr_tail9x9_fwd. */
 int isr_tail9x9_fwd_variant(const isr_tail_desc* d, int32_t variant, isr_stream_t s);
 

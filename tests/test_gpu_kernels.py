@@ -168,7 +168,7 @@ def test_tail9x9(u8):
 def test_tail9x9_persistent_vs_per_tile(n, h, w):
     """Persistent tail variant (one block per CU; (5, 128, 160) has 400 tiles, so blocks
     walk several) vs the production one-tile-per-block kernel, and run-to-run bit equality.
-    The 8-row (3) and row-streaming (4; segment heights 16 / 128 / 32 / 16 here) variants
+    The 8-row (3) and row-streaming (4, 5, 6; segment heights 16 / 128 / 32 / 16 here) variants
     compute the same sums in the same order: bit-identical to the 16-row kernel."""
     import ctypes
     from image_super_resolution_amd import ops, _lib
@@ -190,13 +190,14 @@ def test_tail9x9_persistent_vs_per_tile(n, h, w):
         d8 = ops.tail9x9_desc(xb, wp, b, o8)
         ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(d8), 3, ops._stream()), "tail variant 3")
         torch.cuda.synchronize()
-        os_ = torch.full((n, 3, h, w), 7, device=DEV, dtype=dt)  # row-streaming variant
-        ds = ops.tail9x9_desc(xb, wp, b, os_)
-        ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(ds), 4, ops._stream()), "tail variant 4")
-        torch.cuda.synchronize()
         a, p0, p1 = outs[(dt, 1)][0], outs[(dt, 2)][0], outs[(dt, 2)][1]
         assert torch.equal(o8, a)
-        assert torch.equal(os_, a)
+        for v in (4, 5, 6):  # row-streaming variants (4 and 8 waves, lane-streaming)
+            os_ = torch.full((n, 3, h, w), 7, device=DEV, dtype=dt)
+            ds = ops.tail9x9_desc(xb, wp, b, os_)
+            ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(ds), v, ops._stream()), f"tail variant {v}")
+            torch.cuda.synchronize()
+            assert torch.equal(os_, a), v
         assert torch.equal(p0, p1)
         if dt == torch.float32:
             assert (a - p0).abs().max().item() < 1e-5
