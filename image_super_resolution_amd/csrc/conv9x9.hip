@@ -703,11 +703,12 @@ __global__ __launch_bounds__(256, 1) void tail9x9_stream_kernel(isr_tail_desc d,
         const int u = j * 64 + lane;
         const int p = u / (2 * HC), r = u - p * 2 * HC;
         const int q = r >> 1, c = (r & 1) ^ ((q >> 3) & 1);
-        doff[j] = (uint32_t)((size_t)p * pstride + q * 32 + c * 16);
+        doff[j] = (uint32_t)(p << 16 | (q * 32 + c * 16));  // plane (pstride may exceed 4 GB) | in-plane
     }
     auto dma = [&](int g, int j) {
         const int y = ys - 4 + GR * g + wave;  // within the buffer's zero border (pad 4)
-        glds16(xcol + (ptrdiff_t)y * xrow + doff[j], smem + OFF_IN + ((g % NG) * GR + wave) * ROWB + j * 1024);
+        glds16(xcol + (ptrdiff_t)y * xrow + (size_t)(doff[j] >> 16) * pstride + (doff[j] & 0xffff),
+               smem + OFF_IN + ((g % NG) * GR + wave) * ROWB + j * 1024);
     };
     // the B fragments of the 36 k-steps (chunk, kx, ks), resident for the whole strip
     bf16x8 wr[36];
@@ -930,11 +931,12 @@ __global__ __launch_bounds__(512, 1) void tail9x9_stream8_kernel(isr_tail_desc d
         const int u = j * 64 + lane;
         const int p = u / (2 * HC), r = u - p * 2 * HC;
         const int q = r >> 1, c = (r & 1) ^ ((q >> 3) & 1);
-        doff[j] = (uint32_t)((size_t)p * pstride + q * 32 + c * 16);
+        doff[j] = (uint32_t)(p << 16 | (q * 32 + c * 16));  // plane (pstride may exceed 4 GB) | in-plane
     }
     auto dma = [&](int g, int j) {
         const int y = ys - 4 + GR * g + wave;  // within the buffer's zero border (pad 4)
-        glds16(xcol + (ptrdiff_t)y * xrow + doff[j], smem + OFF_IN + ((g % NG) * GR + wave) * ROWB + j * 1024);
+        glds16(xcol + (ptrdiff_t)y * xrow + (size_t)(doff[j] >> 16) * pstride + (doff[j] & 0xffff),
+               smem + OFF_IN + ((g % NG) * GR + wave) * ROWB + j * 1024);
     };
     bf16x8 wr[36];
 #pragma unroll
