@@ -23,7 +23,7 @@ graph (engine.GraphedPlan; --no-graph for the eager ctypes launch loop, whose
                   rocprofv3's kernel trace of the same command.  traffic = PMC HBM
                   bytes per launch from profiles/<round>_pmc_traffic.json
                   (rocprofv3 --pmc, corrected per MI355X_MICROARCH.md), or null.
-  roofline_kernels — the chain kernel, and the per-conv kernels it is built from
+  roofline_kernels — the chain kernel, the per-conv kernels it is built from, and the 9x9 tail
                   (used by the training path and the non-chained plan), each against
                   its own bound: growth convs (32-cout tile, HBM: (cin + 32) channels x
                   2 B x N*H*W per launch) and the RDB final conv 192->64 (MFMA,
@@ -230,6 +230,21 @@ def main():
                         "frac": round(f_tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic.get("final"),
                         "flops_per_launch": f_flops, "avg_launch_ms": round(f_ms, 5),
                         "launches_per_step": len(f_tags)}
+    # the 9x9 tail (conv2 64->3 + tanh, row-streaming kernel) on the production plan: HBM-bound,
+    # algorithmic bytes = its bf16 input once + the output once
+    p0 = plan.subs[0] if n_streams > 1 else plan
+    t_ms, t_tags = time_family(p0, {("tail9x9", 64, 3)}, stream, sp)
+    hr_side = hw * S
+    t_bytes = (n // max(1, n_streams)) * hr_side * hr_side * (64 * 2 + 3 * out.element_size())
+    t_gbs = t_bytes / (t_ms * 1e-3) / 1e9
+    t_flops = 2.0 * 81 * 64 * 3 * (n // max(1, n_streams)) * hr_side * hr_side
+    kernels["tail"] = {"bound": "hbm", "kernel": "tail9x9 (conv2 9x9 64->3 + tanh, row-streaming, 8 waves)",
+                       "achieved": round(t_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(t_gbs / HBM_PEAK_GBS, 4), "traffic": traffic.get("tail"),
+                       "bytes_per_launch": t_bytes, "avg_launch_ms": round(t_ms, 5),
+                       "launches_per_step": len(t_tags) * max(1, n_streams),
+                       "flops_per_launch": t_flops,
+                       "mfma_frac": round(t_flops / (t_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4)}
     model_flops = engine.generator_flops(hw, hw, args.blocks, S // 2) * n
     f_over_p = model_flops / (MFMA_BF16_PEAK_TFLOPS * 1e12) * 1e3
     b_over_bw = TILE_BYTES * n * (hw * hw) / (128 * 128) / (HBM_PEAK_GBS * 1e9) * 1e3

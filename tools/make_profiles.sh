@@ -13,7 +13,7 @@ P=gpurun_out/profiles_$R   # gpurun merges only gpurun_out/ back (<= 64 MiB); co
 T=/tmp/isr_prof_$R         # raw rocprofv3 output stays off gpurun_out/
 mkdir -p $P $T
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/prof_bench -o bench -- \
-  python3 bench.py --round $R > $P/prof_bench.json 2> $T/prof_bench.err
+  python3 bench.py --round $R > $P/prof_bench.json 2> $P/prof_bench.err
 cp $T/prof_bench/bench_kernel_stats.csv $P/${R}_bench_kernel_stats.csv
 # the dominant kernel (the persistent trunk kernel): its launches from the trace
 python3 - "$T/prof_bench/bench_kernel_trace.csv" "$P/${R}_bench_dominant_by_grid.json" <<'EOF2'
@@ -58,8 +58,8 @@ for k, sub in fam.items():
 json.dump(out, open(f"{P}/{R}_pmc_traffic.json", "w"), indent=1)
 EOF
 cp $P/${R}_pmc_traffic.json profiles/ 2>/dev/null || true
-timeout -k 10 600 python3 bench.py --round $R > $P/${R}_bench.json 2> $T/bench_final.err
+timeout -k 10 600 python3 bench.py --round $R > $P/${R}_bench.json 2> $P/bench_final.err
 cat $P/${R}_bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/prof_train -o train -- \
-  python3 tools/bench_train.py --steps 3 --warmup 2 > $P/${R}_train_bench.json 2> $T/prof_train.err
+  python3 tools/bench_train.py --steps 3 --warmup 2 > $P/${R}_train_bench.json 2> $P/prof_train.err
 cp $T/prof_train/train_kernel_stats.csv $P/${R}_train_kernel_stats.csv
