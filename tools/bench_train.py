@@ -103,13 +103,27 @@ def main():
         torch.distributed.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
     dt = dt.item()
     samples = args.steps * args.batch * world
+    # algorithmic FLOPs of one step per GPU (2*MAC of every conv the step runs):
+    # G fwd (engine.generator_flops) + G bwd (dgrad + wgrad = 2x fwd); VGG19 to conv5_4 on SR
+    # and HR (203.8 GFLOP per 512² image) + its input-gradient on SR; D (49.26 GFLOP per 512²
+    # image, torch FlopCounterMode of models.Discriminator): D(sr) fwd + dgrad for the G loss,
+    # D(sr), D(hr) fwd + dgrad + wgrad for the D loss.  srgan mode only.
+    from image_super_resolution_amd import engine
+    lr = args.hr // 4
+    g_fwd = engine.generator_flops(lr, lr, args.blocks, 2) * args.batch
+    scale = (args.hr / 512) ** 2 * args.batch
+    vgg_fwd, d_fwd = 203.8e9 * scale, 49.26e9 * scale
+    step_flops = (3 * g_fwd + 3 * vgg_fwd + 2 * d_fwd + 2 * d_fwd + 2 * 2 * d_fwd) if args.mode == "srgan" else 3 * g_fwd
+    tflops = step_flops / (dt / args.steps) / 1e12
     if rank == 0:
         print(json.dumps({"metric": f"{args.mode} train step throughput (4x EResNet, VGG19 5_4 L1 + adv)",
                           "value": round(samples * args.hr * args.hr / 1e6 / dt, 2), "unit": "HR MPix/s",
                           "samples_per_s": round(samples / dt, 2), "ms_per_step": round(dt * 1e3 / args.steps, 2),
                           "n_gpus": world, "global_batch": args.batch * world, "steps": args.steps,
                           "discriminator": "miopen" if args.dis_miopen else "libisr",
-                          "mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}), flush=True)
+                          "mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
+                          "tflop_per_step": round(step_flops / 1e12, 2), "tflops_per_s": round(tflops, 1),
+                          "mfma_frac": round(tflops / 2500.0, 4)}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
