@@ -387,11 +387,13 @@ static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
         default:
             if (d->taps == 1) return f(WG<1, 1, 8, 2, 1>());  // stride-2 phase conv: taps {0,1}^2, 4 waves
             // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles; 4-row
-            // stages when cin % 64 == 32 (96, 160), else 16-row stages with 4 waves per kernel
-            // row (12-wave blocks, half the split-K partials): 8-11 % over 8-row stages
+            // stages when cin % 64 == 32 (96, 160), else 8-row stages with 2 waves per kernel
+            // row (variant 5): 4-11 % under the round-1 choice (16-row stages, 4 waves per
+            // row) on cin 64 / 128 / 192 and the sub2 Scaler shape, on two boxes
             if (d->cin % 64 == 32) return f(Fam<4>::C11());
-            if (d->ha % 16 == 0) return f(Fam<16, 4>::C11());
-            return f(Fam<8>::C11());
+            if (d->ha % 8 == 0) return f(Fam<8, 2>::C11());
+            if (d->ha % 4 == 0) return f(Fam<4>::C11());
+            return f(Fam<2>::C11());
     }
 }
 
