@@ -131,6 +131,7 @@ SIGNATURES = {
     "isr_conv3x3_fwd_variant": (c_int32, [POINTER(IsrConvDesc), c_int32, c_void_p]),
     "isr_tuning_conv_stamps": (c_int32, [c_void_p]),
     "isr_tuning_tail_stamps": (c_int32, [c_void_p]),
+    "isr_tuning_chain_knobs": (c_int32, [c_int32, c_int32, c_int32, c_int32]),
     "isr_conv3x3_check": (c_int32, [POINTER(IsrConvDesc)]),
     "isr_conv_chain_state_words": (c_size_t, [c_int32, c_int32, c_int32]),
     "isr_conv_chain": (c_int32, [POINTER(IsrChainDesc), c_void_p]),

@@ -11,6 +11,7 @@ namespace isr {
 int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s);
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s);
 int conv_stamps_set(void* p);
+int chain_knobs_set(const int* k);
 int tail_stamps_set(void* p);
 size_t conv_chain_state_words(int n, int ha, int wa);
 int conv_chain(const isr_chain_desc* c, hipStream_t s);
@@ -236,6 +237,13 @@ int isr_tuning_conv_stamps(void* buf) {
     const int rc = isr::conv_stamps_set(buf);
     if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "conv stamps: library built without -DISR_TUNING");
     return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "conv stamps: hipMemcpyToSymbol failed");
+}
+
+int isr_tuning_chain_knobs(int32_t delay_ticks, int32_t delay_shift, int32_t k2, int32_t k3) {
+    const int k[4] = {delay_ticks, delay_shift, k2, k3};
+    const int rc = isr::chain_knobs_set(k);
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "chain knobs: library built without -DISR_TUNING");
+    return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "chain knobs: hipMemcpyToSymbol failed");
 }
 
 int isr_tuning_tail_stamps(void* buf) {

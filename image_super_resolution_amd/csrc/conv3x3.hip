@@ -52,7 +52,7 @@ __device__ __forceinline__ void conv_stamp(int slot, int row = -1) {
 }
 
 template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1), int EPQ_ = 4,
-          int SPL_ = 0, int TWN_ = 0>
+          int SPL_ = 0, int TWN_ = 0, int NSW_ = 0>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
     // 1: double-buffered fragment registers across (k-step, dx) steps; 2: the next step's reads
@@ -87,10 +87,20 @@ struct C3 {
     static constexpr int INSTR = HALO_INSTR + W_INSTR;
     static constexpr int IPW = (INSTR + WM - 1) / WM; // glds per wave per chunk (uniform)
     static constexpr int STAGE = IPW * WM * 1024;
+    // NSW > 0: separate rings — halo planes NST deep (NST-1 chunks in flight), weights NSW deep
+    // (one chunk ahead): the growth convs keep two halo chunks in flight at two blocks per CU
+    static constexpr int NSW = NSW_;
+    static constexpr int IPWH = (HALO_INSTR + WM - 1) / WM; // halo glds per wave per chunk
+    static constexpr int IPWW = (W_INSTR + WM - 1) / WM;    // weight glds per wave (the last
+                                                            // round repeats pieces: same bytes)
+    static constexpr int HSTAGE = HALO_INSTR * 1024;
+    static constexpr int WSTAGE = W_INSTR * 1024;
+    static constexpr int RING = NSW ? NST * HSTAGE + NSW * WSTAGE : NST * STAGE;
     static constexpr int NT = 64 * WM;
     static constexpr int EPS = CT + 4;                 // floats per pixel in the epilogue image
     static constexpr int EP_BYTES = WM * 32 * EPS * 4; // one output row per wave at a time
-    static constexpr int LDS = (NST * STAGE > EP_BYTES) ? NST * STAGE : EP_BYTES;
+    static constexpr int LDS = (RING > EP_BYTES) ? RING : EP_BYTES;
+    static_assert(!NSW || (HALO_INSTR % WM == 0 && NST >= 3 && NSW == 2), "split rings");
     static constexpr int BPC = 163840 / LDS; // blocks per CU by LDS
     static constexpr int OCC = BPC * WM / 4 >= 2 ? 2 : 1; // waves per SIMD to budget registers for
     static_assert(LDS <= 163840, "LDS budget");
@@ -256,8 +266,17 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
 // described by `d`, computed by the whole workgroup.  HX = 1 (the persistent chain kernel,
 // conv_chain.hip): activations written by other workgroups of the same launch are read with
 // sc1 loads (L1 bypass) and the outputs stored write-through (sc1), Guideline 16's hand-off.
-template <class C, bool XS2, int HX, class Desc>
-__device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1) {
+struct NoPre {
+    __device__ void operator()() const {}
+};
+
+// pre(): run after the tile's scalar setup (descriptor loads, addresses, bias loads) is issued
+// and before its first LDS-DMA (the chain's dependency wait: the setup's memory latency then
+// overlaps the wait); with early0 the first NST-1 chunks are staged before pre() (the chain,
+// when those input channels were not written by the previous layer).
+template <class C, bool XS2, int HX, class Desc, class Pre = NoPre>
+__device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, const Pre& pre = Pre{},
+                                          bool early0 = false) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int R = C::R, NF = C::NF, WM = C::WM;
 
@@ -317,6 +336,31 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1) {
         return o;
     };
 
+    // split rings (NSW): halo pieces j = wave + WM*k (k < IPWH) and weight pieces jj = (wave + WM*k) %
+    // W_INSTR (k < IPWW; the wrap repeats a piece: the same bytes to the same LDS address)
+    auto stage_h = [&](int chunk, int buf) {
+        char* dst = smem + buf * C::HSTAGE;
+        const char* xs = xbase + xchunk(chunk);
+#pragma unroll
+        for (int k = 0; k < C::IPWH; ++k) {
+            const int j = wave + WM * k;
+            const uint32_t o = off_of(k);
+            if constexpr (HX) glds16_sc1(xs + o, dst + j * 1024);
+            else glds16(xs + o, dst + j * 1024);
+        }
+    };
+    auto stage_w = [&](int chunk, int buf) {
+        char* dst = smem + C::NST * C::HSTAGE + buf * C::WSTAGE;
+        const char* ws = wbase + (size_t)chunk * wchunk_bytes;
+#pragma unroll
+        for (int k = 0; k < C::IPWW; ++k) {
+            const int jj = (wave + WM * k) % C::W_INSTR;
+            const int u = jj * 64 + lane;
+            const int seg = u / (C::CT * 2);
+            const int rem = u - seg * (C::CT * 2);
+            glds16(ws + (uint32_t)((seg * d.cout + ct * C::CT) * 32 + rem * 16), dst + jj * 1024);
+        }
+    };
     auto stage = [&](int chunk, int buf, int k0 = 0, int k1 = C::IPW) {
         char* dst = smem + buf * C::STAGE;
         const char* xs = xbase + xchunk(chunk);
@@ -347,14 +391,37 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1) {
         for (int r = 0; r < R; ++r) acc[r][f] = b0;
     }
 
+    auto prologue = [&]() {
+        if constexpr (C::NSW) {  // issue order h(0), w(0), h(1), ..., h(NST-2): see the chunk wait
+            stage_h(0, 0);
+            stage_w(0, 0);
 #pragma unroll
-    for (int s = 0; s < C::NST - 1; ++s)
-        if (s < nchunks) stage(s, s);
+            for (int s = 1; s < C::NST - 1; ++s)
+                if (s < nchunks) stage_h(s, s);
+        } else {
+#pragma unroll
+            for (int s = 0; s < C::NST - 1; ++s)
+                if (s < nchunks) stage(s, s);
+        }
+    };
+    if (early0) prologue();
+    pre();
+    if (!early0) prologue();
+    conv_stamp(5, srow);
 
     const int qw = wave * R * C::HC + l31; // halo pixel of (row w*R, col l31)
     for (int chunk = 0; chunk < nchunks; ++chunk) {
         // chunk `chunk` landed for this wave: younger chunks in flight = min(NST-2, nchunks-1-chunk)
-        if constexpr (C::NST >= 3) {
+        if constexpr (C::NSW) {
+            // issue order ... w(c-1) h(c+1) | w(c) h(c+2) ...: at chunk c only the halo pieces of
+            // chunk c+1 (issued after w(c)) may still be in flight (NST == 3)
+            static_assert(C::NSW == 0 || C::NST == 3, "split-ring wait assumes NST 3");
+            if (chunk + 1 < nchunks) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::IPWH) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        } else if constexpr (C::NST >= 3) {
             if (chunk + C::NST - 2 < nchunks) {
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"((C::NST - 2) * C::IPW) : "memory");
             } else {
@@ -367,12 +434,20 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1) {
         __builtin_amdgcn_s_barrier();
         if (chunk == 0) conv_stamp(1, srow);
         const bool refill = !(C::ABL & 2) && chunk + C::NST - 1 < nchunks;
+        // split rings: w(chunk+1) then h(chunk+NST-1), each when it exists
+        auto refill_split = [&]() {
+            if (chunk + 1 < nchunks) stage_w(chunk + 1, (chunk + 1) % C::NSW);
+            if (refill) stage_h(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+        };
         if constexpr (C::SPL == 1 || (C::SPL == 0 && C::PIPE != 2)) {
-            if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+            if constexpr (C::NSW) refill_split();
+            else if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
         }
 
-        const char* hs = smem + ((C::ABL & 2) ? 0 : (chunk % C::NST)) * C::STAGE;
-        const char* ws = hs + C::HALO_INSTR * 1024;
+        const char* hs = C::NSW ? smem + (chunk % C::NST) * C::HSTAGE
+                                : smem + ((C::ABL & 2) ? 0 : (chunk % C::NST)) * C::STAGE;
+        const char* ws = C::NSW ? smem + C::NST * C::HSTAGE + (chunk % (C::NSW ? C::NSW : 1)) * C::WSTAGE
+                                : hs + C::HALO_INSTR * 1024;
         // Software pipeline over the chunk's (k-step, dx) steps: the fragments of
         // step st+1 are read into the other register set while step st's MFMAs
         // run, so LDS latency is covered by MFMA work of the same wave.
@@ -416,7 +491,8 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1) {
             // step 0's fragment reads are in flight, instead of ahead of them
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (C::SPL == 0) {
-                if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+                if constexpr (C::NSW) refill_split();
+                else if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -642,6 +718,39 @@ struct ChainArgs {
 };
 
 #define CHAIN_STAMP_L0 75  // tuning stamps: the 15 layers of RRDB 5
+// chain stamp rows start past every per-conv launch's blockIdx rows (those stamp at row
+// blockIdx.x: up to 8192 for the x4 Scaler), so the later launches of a forward cannot
+// overwrite them
+#define CHAIN_STAMP_BASE 65536
+
+#ifdef ISR_TUNING
+// isr_tuning_chain_knobs: [0] start delay (s_memrealtime ticks, 100 MHz) of the workgroups whose
+// bit [1] of blockIdx.x is set (a phase offset between independent image groups)
+__device__ int g_chain_knobs[4];
+#endif
+
+__device__ __forceinline__ void chain_tuning_prologue(int ntiles) {
+#ifdef ISR_TUNING
+    unsigned long long* p = g_conv_stamps;
+    if (p != nullptr && threadIdx.x == 0) {  // placement of every workgroup, after the 15 stamped layers
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20); // HW_REG_XCC_ID
+        p[((size_t)CHAIN_STAMP_BASE + 15 * ntiles + blockIdx.x) * 8 + 6] = hw;
+        p[((size_t)CHAIN_STAMP_BASE + 15 * ntiles + blockIdx.x) * 8 + 7] = xcc;
+    }
+    const int dly = g_chain_knobs[0];
+    if (dly > 0 && ((blockIdx.x >> g_chain_knobs[1]) & 1)) {
+        unsigned long long t0, t;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+        do {
+            __builtin_amdgcn_s_sleep(8);
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        } while (t - t0 < (unsigned long long)dly);
+    }
+#else
+    (void)ntiles;
+#endif
+}
 
 __global__ void chain_bump_kernel(unsigned* state) {
     if (threadIdx.x == 0) state[threadIdx.x] = state[threadIdx.x] + 1u;  // vector store by lane 0
@@ -690,24 +799,44 @@ typedef const __attribute__((address_space(4))) isr_conv_desc const_desc;  // co
 // layer order (no residency assumption) measured slower: 9.3 vs 6.8 ms per forward — it
 // rebuilds a per-layer front and loses that locality.  All G workgroups must be resident
 // (G <= 2 per CU); a wait that never completes gives up (bounded) instead of hanging.
-template <class CG, class CF>
-__global__ __launch_bounds__(256, 2) void conv_chain_kernel(ChainArgs a) {
+// WM_: 0 = dependency wait before the tile; 1 = inside conv_tile after its scalar setup (the
+// descriptor loads overlap the wait); 2 = as 1, and the first chunk is staged before the wait
+// when the previous layer did not write those input channels (every layer but an RDB's first)
+template <class CG, class CF, int WM_ = 0>
+__global__ __launch_bounds__(CG::NT, 2) void conv_chain_kernel(ChainArgs a) {
     // bumped by chain_bump_kernel before this launch; an agent-scope load, so no CU reads a
     // stale copy of another XCD's write
     const unsigned gen = __hip_atomic_load(a.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    chain_tuning_prologue(a.ntiles);
     for (int L = 0; L < a.nl; ++L) {
         const_desc& d = ((const_desc*)(uintptr_t)a.layers)[L];
         const int kind = a.kinds[L];
         for (int t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
 #ifdef ISR_TUNING
-            const int srow = (L >= CHAIN_STAMP_L0 && L < CHAIN_STAMP_L0 + 15) ? (L - CHAIN_STAMP_L0) * a.ntiles + t : -2;
+            const int srow =
+                (L >= CHAIN_STAMP_L0 && L < CHAIN_STAMP_L0 + 15) ? CHAIN_STAMP_BASE + (L - CHAIN_STAMP_L0) * a.ntiles + t : -2;
 #else
             const int srow = -2;
 #endif
             conv_stamp(4, srow);  // wait start
-            if (L > 0) chain_wait(a, t, gen * 1024u + (unsigned)L, gen);
-            if (kind == 0) conv_tile<CG, false, 1>(d, t, srow);
-            else conv_tile<CF, false, 1>(d, t, srow);
+            if constexpr (WM_ == 0) {
+                if (L > 0) chain_wait(a, t, gen * 1024u + (unsigned)L, gen);
+                if (kind == 0) conv_tile<CG, false, 1>(d, t, srow);
+                else conv_tile<CF, false, 1>(d, t, srow);
+            } else {
+                bool early0 = false;
+                if (WM_ == 2 && L > 0) {
+                    // first-chunk input channels [x.coff, x.coff + 16) vs the previous layer's output
+                    const_desc& dp = ((const_desc*)(uintptr_t)a.layers)[L - 1];
+                    const int ech = 16 * (kind == 0 ? CG::NST - 1 : CF::NST - 1);  // channels staged early
+                    early0 = !(dp.y.data == d.x.data && dp.y.coff < d.x.coff + ech && d.x.coff < dp.y.coff + dp.cout);
+                }
+                auto pre = [&]() {
+                    if (L > 0) chain_wait(a, t, gen * 1024u + (unsigned)L, gen);
+                };
+                if (kind == 0) conv_tile<CG, false, 1>(d, t, srow, pre, early0);
+                else conv_tile<CF, false, 1>(d, t, srow, pre, early0);
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores are done
             conv_stamp(3, srow);
             __syncthreads();
@@ -723,33 +852,73 @@ size_t conv_chain_state_words(int n, int ha, int wa) {
     return (tiles + 4 + 3) / 4 * 4;  // [0] fail word, [4..] progress; a multiple of 16 bytes
 }
 
-int conv_chain(const isr_chain_desc* c, hipStream_t s) {
-    static_assert(V_G0::TH == V_F0::TH && V_G0::TW == V_F0::TW, "one tile grid");
-    static_assert(V_G0::NT == 256 && V_F0::NT == 256, "chain block size");
+#ifdef ISR_TUNING
+static int g_chain_variant_host = 0;  // isr_tuning_chain_knobs k2: chain kernel variant (A/B only)
+#endif
+
+template <class CG, class CF, int WM_ = 0>
+static int launch_chain(const isr_chain_desc* c, hipStream_t s) {
+    static_assert(CG::TH == CF::TH && CG::TW == CF::TW, "one tile grid");
+    static_assert(CG::NT == CF::NT, "one block size");
+    if (c->ha % CG::TH || c->wa % CG::TW) return -2;
     ChainArgs a;
     a.layers = c->layers;
     a.kinds = c->kinds;
     a.nl = c->nl;
-    a.nby = c->ha / V_G0::TH;
-    a.nbx = c->wa / V_G0::TW;
+    a.nby = c->ha / CG::TH;
+    a.nbx = c->wa / CG::TW;
     a.ntiles = c->n * a.nby * a.nbx;
     a.state = c->state;
     a.acquire = c->acquire;
     if (c->nl >= 1024) return -2;
     hipLaunchKernelGGL(chain_bump_kernel, dim3(1), dim3(64), 0, s, c->state);
-    auto kern = conv_chain_kernel<V_G0, V_F0>;
-    constexpr int lds = V_G0::LDS > V_F0::LDS ? V_G0::LDS : V_F0::LDS;
+    auto kern = conv_chain_kernel<CG, CF, WM_>;
+    constexpr int lds = CG::LDS > CF::LDS ? CG::LDS : CF::LDS;
+    constexpr int per_cu = 163840 / lds < 2 ? 163840 / lds : 2;  // the kernel's occupancy (<= 2 by registers)
     lds_limit((const void*)kern, lds);
-    const int slots = 2 * cu_count();  // every workgroup resident: 2 per CU (the kernel's occupancy)
+    const int slots = per_cu * cu_count();  // every workgroup resident
     const int grid = a.ntiles < slots ? a.ntiles : slots;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(CG::NT), lds, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int conv_chain(const isr_chain_desc* c, hipStream_t s) {
+#ifdef ISR_TUNING
+    switch (g_chain_variant_host) {
+        case 1:  // RDB final conv: every residual unit of a pass loaded at once (EPQ 8)
+            return launch_chain<V_G0, C3<4, 4, 2, 16, 2, 192, 0, 2, 8>>(c, s);
+        case 2:  // 32x32 tiles, 8 waves, 1 block / CU: growth 3-deep ring, final 2-deep
+            return launch_chain<C3<4, 8, 1, 16, 3, 0, 0, 2>, C3<4, 8, 2, 16, 2, 192, 0, 2>>(c, s);
+        case 3:  // 2 + EPQ 8
+            return launch_chain<C3<4, 8, 1, 16, 3, 0, 0, 2>, C3<4, 8, 2, 16, 2, 192, 0, 2, 8>>(c, s);
+        case 4:  // 32x32 tiles, both 2-deep
+            return launch_chain<C3<4, 8, 1, 16, 2, 0, 0, 2>, C3<4, 8, 2, 16, 2, 192, 0, 2>>(c, s);
+        case 7:  // growth convs: split rings (halo 3 deep, weights 2 deep), wait after setup
+            return launch_chain<C3<4, 4, 1, 16, 3, 0, 0, 2, 4, 0, 0, 2>, V_F0, 1>(c, s);
+        case 8:  // 7 with the wait before the tile
+            return launch_chain<C3<4, 4, 1, 16, 3, 0, 0, 2, 4, 0, 0, 2>, V_F0, 0>(c, s);
+        case 5:  // the wait before the tile (the round-2 form; production waits after the setup)
+            return launch_chain<V_G0, V_F0, 0>(c, s);
+        case 6:  // 5 + first chunk staged before the wait where independent of the previous layer
+            return launch_chain<V_G0, V_F0, 2>(c, s);
+        default: break;
+    }
+#endif
+    // production: the dependency wait runs after the tile's scalar setup (its descriptor loads —
+    // three dependent scalar round trips, ~2.4 µs per tile — overlap the wait): -1.2 % per
+    // forward against waiting first (tools/chain_probe.py, variant 0 vs 5)
+    return launch_chain<V_G0, V_F0, 1>(c, s);
 }
 
 #ifdef ISR_TUNING
 int conv_stamps_set(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_conv_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+int chain_knobs_set(const int* k) {
+    g_chain_variant_host = k[2];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_chain_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
+}
 #else
 int conv_stamps_set(void*) { return -2; }
+int chain_knobs_set(const int*) { return -2; }
 #endif
 
 int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) {

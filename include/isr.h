@@ -319,6 +319,11 @@ int isr_tuning_conv_stamps(void* buf);
  * 36 = 4 with stamps) into `buf` (4 x uint64 per (block, wave): entry, exit, summed
  * top-of-row-group wait + barrier, summed loop; s_memrealtime ticks); NULL stops. */
 int isr_tuning_tail_stamps(void* buf);
+/* Tuning builds only: persistent-chain probes for later isr_conv_chain launches —
+ * workgroups with bit `delay_shift` of their index set start `delay_ticks` (100 MHz) late;
+ * k2 = chain kernel variant for later launches (0 = production; A/B only); k3 reserved (0).
+ * A default build returns ISR_ERR_UNSUPPORTED. */
+int isr_tuning_chain_knobs(int32_t delay_ticks, int32_t delay_shift, int32_t k2, int32_t k3);
 /* Validation only: ISR_OK when isr_conv3x3_fwd would accept `d` (nothing launched). */
 int isr_conv3x3_check(const isr_conv_desc* d);
 

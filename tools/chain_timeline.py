@@ -17,6 +17,7 @@ from image_super_resolution_amd import _lib, engine, models  # noqa: E402
 from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_state_dict  # noqa: E402
 
 L0 = 75
+BASE = 65536  # CHAIN_STAMP_BASE in conv3x3.hip
 
 
 def pct(v, qs=(0.1, 0.5, 0.9, 1.0)):
@@ -26,6 +27,8 @@ def pct(v, qs=(0.1, 0.5, 0.9, 1.0)):
 
 def main():
     lib = _lib.load()
+    variant = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    _lib.check(lib.isr_tuning_chain_knobs(0, 0, variant, 0), "knobs")
     dev = torch.device("cuda")
     sd = synth_state_dict(models.ResNet(16, 0.2, scaleRate=4).state_dict(), seed=0)
     gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev)
@@ -37,19 +40,20 @@ def main():
     for _ in range(3):
         plan.run(x, out)
     torch.cuda.synchronize()
-    ntiles = 512
-    st = torch.zeros(15 * ntiles * 8, dtype=torch.int64, device=dev)
+    ntiles = plan.chain.ntiles if hasattr(plan.chain, 'ntiles') else (256 if variant in (2, 3, 4) else 512)
+    st = torch.zeros((BASE + 15 * ntiles) * 8, dtype=torch.int64, device=dev)
     _lib.check(lib.isr_tuning_conv_stamps(ctypes.c_void_p(st.data_ptr())), "stamps")
     plan.run(x, out)
     torch.cuda.synchronize()
     _lib.check(lib.isr_tuning_conv_stamps(None), "stamps off")
-    a = st.view(15, ntiles, 8).cpu().double() / 100.0  # 100 MHz ticks -> us
+    a = st.view(-1, 8)[BASE:].view(15, ntiles, 8).cpu().double() / 100.0  # 100 MHz ticks -> us
     t0 = a[0, :, 4].min().item()
     for L in range(15):
         w0, e, c0, m, dn = a[L, :, 4], a[L, :, 0], a[L, :, 1], a[L, :, 2], a[L, :, 3]
         row = {"layer": L0 + L, "kind": "final" if L % 5 == 4 else f"growth{L % 5}",
                "start_p10..max": pct((w0 - t0).tolist()), "end_p10..max": pct((dn - t0).tolist()),
-               "wait": pct((e - w0).tolist()), "prologue": pct((c0 - e).tolist()),
+               "wait": pct((e - w0).tolist()), "setup": pct((a[L, :, 5] - e).tolist()),
+               "dma0": pct((c0 - a[L, :, 5]).tolist()), "prologue": pct((c0 - e).tolist()),
                "main": pct((m - c0).tolist()), "epi+drain": pct((dn - m).tolist()),
                "tile_total": pct((dn - w0).tolist())}
         print(json.dumps(row), flush=True)
