@@ -801,13 +801,24 @@ typedef const __attribute__((address_space(4))) isr_conv_desc const_desc;  // co
 // (G <= 2 per CU); a wait that never completes gives up (bounded) instead of hanging.
 // WM_: 0 = dependency wait before the tile; 1 = inside conv_tile after its scalar setup (the
 // descriptor loads overlap the wait); 2 = as 1, and the first chunk is staged before the wait
-// when the previous layer did not write those input channels (every layer but an RDB's first)
+// when the previous layer did not write those input channels (every layer but an RDB's first);
+// 3 = as 1, and a tile's store drain + progress publish is deferred into the NEXT tile's pre(),
+// after that tile's scalar setup (the write-through drain overlaps the setup's latency)
 template <class CG, class CF, int WM_ = 0>
 __global__ __launch_bounds__(CG::NT, 2) void conv_chain_kernel(ChainArgs a) {
     // bumped by chain_bump_kernel before this launch; an agent-scope load, so no CU reads a
     // stale copy of another XCD's write
     const unsigned gen = __hip_atomic_load(a.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     chain_tuning_prologue(a.ntiles);
+    int pend_t = -1;  // WM_ 3: tile whose stores are not yet drained / published (uniform)
+    unsigned pend_v = 0;
+    auto publish_pending = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores are done
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(a.state + 4 + pend_t, pend_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend_t = -1;
+    };
     for (int L = 0; L < a.nl; ++L) {
         const_desc& d = ((const_desc*)(uintptr_t)a.layers)[L];
         const int kind = a.kinds[L];
@@ -832,10 +843,16 @@ __global__ __launch_bounds__(CG::NT, 2) void conv_chain_kernel(ChainArgs a) {
                     early0 = !(dp.y.data == d.x.data && dp.y.coff < d.x.coff + ech && d.x.coff < dp.y.coff + dp.cout);
                 }
                 auto pre = [&]() {
+                    if (WM_ == 3 && pend_t >= 0) publish_pending();
                     if (L > 0) chain_wait(a, t, gen * 1024u + (unsigned)L, gen);
                 };
                 if (kind == 0) conv_tile<CG, false, 1>(d, t, srow, pre, early0);
                 else conv_tile<CF, false, 1>(d, t, srow, pre, early0);
+                if constexpr (WM_ == 3) {
+                    pend_t = t;
+                    pend_v = gen * 1024u + (unsigned)(L + 1);
+                    continue;
+                }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores are done
             conv_stamp(3, srow);
@@ -845,6 +862,7 @@ __global__ __launch_bounds__(CG::NT, 2) void conv_chain_kernel(ChainArgs a) {
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    if (pend_t >= 0) publish_pending();
 }
 
 size_t conv_chain_state_words(int n, int ha, int wa) {
@@ -893,6 +911,8 @@ int conv_chain(const isr_chain_desc* c, hipStream_t s) {
             return launch_chain<C3<4, 8, 1, 16, 3, 0, 0, 2>, C3<4, 8, 2, 16, 2, 192, 0, 2, 8>>(c, s);
         case 4:  // 32x32 tiles, both 2-deep
             return launch_chain<C3<4, 8, 1, 16, 2, 0, 0, 2>, C3<4, 8, 2, 16, 2, 192, 0, 2>>(c, s);
+        case 9:  // deferred drain + publish (WM 3)
+            return launch_chain<V_G0, V_F0, 3>(c, s);
         case 7:  // growth convs: split rings (halo 3 deep, weights 2 deep), wait after setup
             return launch_chain<C3<4, 4, 1, 16, 3, 0, 0, 2, 4, 0, 0, 2>, V_F0, 1>(c, s);
         case 8:  // 7 with the wait before the tile

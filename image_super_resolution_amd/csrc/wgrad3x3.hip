@@ -39,15 +39,20 @@ __device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int NCO_, int NCI_, int TY_, int KW_ = 1, int TWN_ = 0>
+template <int NCO_, int NCI_, int TY_, int KW_ = 1, int TWN_ = 0, int CW_ = 1>
 struct WG {
     static constexpr int NCO = NCO_, NCI = NCI_, TY = TY_;
+    // CW waves per (kernel row, K-share) split the block's NCI ci tiles between them: the block
+    // stages each pixel tile's G and X planes ONCE for all its ci tiles (CW = NCI: every 32-ci
+    // tile of the layer in one block, so G is not re-staged per ci tile)
+    static constexpr int CW = CW_, NCIW = NCI_ / CW_;
     // tap window: 0 = 3x3; 1 = taps {0,1}^2 (2 kernel rows, 2 columns: stride-2 phase convs)
     static constexpr int TWN = TWN_, TN = TWN_ ? 2 : 3;
     // KW waves per kernel row dy split each stage's K (pixel groups) between them;
     // their partial sums are added through LDS before the workspace store
     static constexpr int KW = KW_;
-    static constexpr int WM = TN * KW, NT = 64 * WM;
+    static constexpr int WM = TN * KW * CW, NT = 64 * WM;
+    static_assert(NCI % CW == 0, "ci tiles split evenly between the CW waves");
     static constexpr int CO_T = 32 * NCO, CI_T = 32 * NCI;
     static constexpr int GPL = 2 * NCO, XPL = 2 * NCI;         // 16-channel planes per stage
     static constexpr int XPIX = (TY + 2) * 34;                  // halo pixels per plane
@@ -61,7 +66,7 @@ struct WG {
     static constexpr int STAGE = G_BYTES + XPL * X_PLANE;
     static constexpr int G_INSTR = GPL * G_IPL, INSTR = G_INSTR + XPL * X_IPL;
     static constexpr int IPW = (INSTR + WM - 1) / WM;
-    static constexpr int RED = (KW - 1) * TN * 64 * (TN * NCO * NCI * 16 + NCO) * 4;  // cross-wave K reduction
+    static constexpr int RED = CW * (KW - 1) * TN * 64 * (TN * NCO * NCIW * 16 + NCO) * 4;  // cross-wave K reduction
     static constexpr int LDS = 2 * STAGE > RED ? 2 * STAGE : RED;
     static_assert(LDS <= 163840, "LDS budget");
     static_assert((2 * TY) % KW == 0, "K groups split evenly between the KW waves of a row");
@@ -85,7 +90,9 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
     const int split = b;
     const int t0 = (int)((long)split * a.tiles / a.splits), t1 = (int)((long)(split + 1) * a.tiles / a.splits);
     const int wave = wave_id();
-    const int dy = wave % C::TN, kh = wave / C::TN;  // kernel row, K-share of this wave
+    const int dy = wave % C::TN, kh = (wave / C::TN) % C::KW;  // kernel row, K-share of this wave
+    const int cw = wave / (C::TN * C::KW);                       // ci-tile group of this wave
+    constexpr int NCIW = C::NCIW;
     const int lane = threadIdx.x & 63;
     const int nbx = d.wa / 32, nby = d.ha / TY;
 
@@ -151,19 +158,19 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         }
     };
 
-    f32x16 acc[C::TN][NCO][NCI];
+    f32x16 acc[C::TN][NCO][NCIW];
 #pragma unroll
     for (int dx = 0; dx < C::TN; ++dx)
 #pragma unroll
         for (int f = 0; f < NCO; ++f)
 #pragma unroll
-            for (int e = 0; e < NCI; ++e)
+            for (int e = 0; e < NCIW; ++e)
 #pragma unroll
                 for (int g = 0; g < 16; ++g) acc[dx][f][e][g] = 0.f;
     float bsum[NCO];
 #pragma unroll
     for (int f = 0; f < NCO; ++f) bsum[f] = 0.f;
-    const bool do_bias = d.db && cit == 0 && dy == 1;
+    const bool do_bias = d.db && cit == 0 && dy == 1 && cw == 0;
 
     // transposed-read lane geometry: plane gi of the 32-channel fragment, pixel q + 8h, channels 4p..4p+3
     const int gi = (lane >> 4) & 1, hh = lane >> 5, q = (lane >> 2) & 3, p = lane & 3;
@@ -196,16 +203,16 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
             }
 #pragma unroll
             for (int dx = 0; dx < C::TN; ++dx) {
-                bf16x8 fb[NCI];
+                bf16x8 fb[NCIW];
 #pragma unroll
-                for (int e = 0; e < NCI; ++e) {
-                    const char* pb = base + b_lane + 2 * e * C::X_PLANE + ((r + dy) * 34 + c0 + dx) * 32;
+                for (int e = 0; e < NCIW; ++e) {
+                    const char* pb = base + b_lane + 2 * (cw * NCIW + e) * C::X_PLANE + ((r + dy) * 34 + c0 + dx) * 32;
                     fb[e] = cat4(lds_tr4(pb), lds_tr4(pb + 4 * 32));
                 }
 #pragma unroll
                 for (int f = 0; f < NCO; ++f)
 #pragma unroll
-                    for (int e = 0; e < NCI; ++e) acc[dx][f][e] = mfma32(fa[f], fb[e], acc[dx][f][e]);
+                    for (int e = 0; e < NCIW; ++e) acc[dx][f][e] = mfma32(fa[f], fb[e], acc[dx][f][e]);
             }
         }
     }
@@ -214,17 +221,17 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         // add the K-shares of the KW waves of each kernel row (through the now idle stage LDS)
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __syncthreads();
-        constexpr int PER = C::TN * NCO * NCI * 16 + NCO;  // floats per lane
+        constexpr int PER = C::TN * NCO * NCIW * 16 + NCO;  // floats per lane
         float* red = reinterpret_cast<float*>(smem);
         if (kh > 0) {
-            float* dst = red + ((size_t)((kh - 1) * C::TN + dy) * 64 + lane) * PER;
+            float* dst = red + ((size_t)((cw * (C::KW - 1) + kh - 1) * C::TN + dy) * 64 + lane) * PER;
             int q = 0;
 #pragma unroll
             for (int dx = 0; dx < C::TN; ++dx)
 #pragma unroll
                 for (int f = 0; f < NCO; ++f)
 #pragma unroll
-                    for (int e = 0; e < NCI; ++e)
+                    for (int e = 0; e < NCIW; ++e)
 #pragma unroll
                         for (int g = 0; g < 16; ++g) dst[q++] = acc[dx][f][e][g];
 #pragma unroll
@@ -234,14 +241,14 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
         if (kh > 0) return;
 #pragma unroll
         for (int k = 1; k < C::KW; ++k) {
-            const float* src = red + ((size_t)((k - 1) * C::TN + dy) * 64 + lane) * PER;
+            const float* src = red + ((size_t)((cw * (C::KW - 1) + k - 1) * C::TN + dy) * 64 + lane) * PER;
             int q = 0;
 #pragma unroll
             for (int dx = 0; dx < C::TN; ++dx)
 #pragma unroll
                 for (int f = 0; f < NCO; ++f)
 #pragma unroll
-                    for (int e = 0; e < NCI; ++e)
+                    for (int e = 0; e < NCIW; ++e)
 #pragma unroll
                         for (int g = 0; g < 16; ++g) acc[dx][f][e][g] += src[q++];
 #pragma unroll
@@ -258,15 +265,15 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
 #pragma unroll
         for (int f = 0; f < NCO; ++f)
 #pragma unroll
-            for (int e = 0; e < NCI; ++e)
+            for (int e = 0; e < NCIW; ++e)
 #pragma unroll
                 for (int g = 0; g < 16; ++g) {
                     const int co = cot * C::CO_T + f * 32 + (g & 3) + 8 * (g >> 2) + 4 * hh;
-                    const int ci = cit * C::CI_T + e * 32 + l31;
+                    const int ci = cit * C::CI_T + (cw * NCIW + e) * 32 + l31;
                     wt[(size_t)co * d.cin + ci] = acc[dx][f][e][g];
                 }
     }
-    if (d.db && cit == 0 && dy == 1) {
+    if (d.db && cit == 0 && dy == 1 && cw == 0) {
         float* bp = wsp + (size_t)9 * d.cout * d.cin;
 #pragma unroll
         for (int f = 0; f < NCO; ++f) {
@@ -328,9 +335,10 @@ struct Fam {
     using C11 = WG<1, 1, TY, KW>;
 };
 
-static int wgrad_splits(const isr_wgrad_desc* d, int tiles, int pairs, int target) {
+static int wgrad_splits(const isr_wgrad_desc* d, int tiles, int pairs, int target, int min_splits = 1) {
     if (d->splits > 0) return d->splits < tiles ? d->splits : tiles;
     int s = (target + pairs - 1) / pairs;
+    if (s < min_splits) s = min_splits;
     return s < tiles ? s : tiles;
 }
 
@@ -339,8 +347,14 @@ static void wgrad_geometry(const isr_wgrad_desc* d, int* tiles, int* splits) {
     *tiles = d->n * (d->ha / C::TY) * (d->wa / 32);
     // ~640 blocks of <= 6 waves; blocks with more K-share waves need proportionally fewer
     // splits (each split-K partial costs a workspace write + reduce read)
-    const int target = C::KW > 2 ? 640 * 2 / C::KW : 640;
-    *splits = wgrad_splits(d, *tiles, (d->cout / C::CO_T) * (d->cin / C::CI_T), target);
+    // CW > 1 (all of a layer's ci tiles in one block, up to 15 waves): ~2 blocks per CU slot.
+    // KW == 2 (8-row stages): ~512 blocks and >= 64 splits — the split-K sweep
+    // (tools/tune_wgrad.py --splits, profiles/r02_wgrad_splits.jsonl) put the best split count
+    // at 128-256 for 2-4 (co, ci) tile pairs and at 64 for 12-16 pairs: 6-20 % under the
+    // earlier ~640-block target, whose extra partials cost more in the reduce than they gain
+    const int target = C::CW > 1 ? (C::LDS > 81920 ? 512 : 1024) / (C::CO_T == 64 && d->cin > C::CI_T ? 2 : 1)
+                                 : (C::KW > 2 ? 640 * 2 / C::KW : (C::KW == 2 ? 512 : 640));
+    *splits = wgrad_splits(d, *tiles, (d->cout / C::CO_T) * (d->cin / C::CI_T), target, C::KW == 2 ? 64 : 1);
 }
 
 template <class C>
@@ -370,9 +384,40 @@ static auto pick_in(const isr_wgrad_desc* d, bool co1, F&& f) {
     return f(typename Fm::C11());
 }
 
+// ci-split forms (WG CW > 1): every ci tile of the layer (or half of them at cout 64 / cin 192)
+// in one block, so each pixel tile's G and X planes are staged once per block
+template <int TY, class F>
+static auto pick_cw(const isr_wgrad_desc* d, F&& f, bool* ok) {
+    *ok = true;
+    if (d->taps == 0 && !d->x_sub2) {
+        if (d->cout % 64 != 0) {  // cout 32 (growth convs)
+            switch (d->cin) {
+                case 64: return f(WG<1, 2, TY, 1, 0, 2>());
+                case 96: return f(WG<1, 3, 4, 1, 0, 3>());
+                case 128: return f(WG<1, 4, 4, 1, 0, 4>());
+                case 160: return f(WG<1, 5, 4, 1, 0, 5>());
+                default: break;
+            }
+        } else if (d->cin == 192) {
+            return f(WG<2, 3, 4, 1, 0, 3>());
+        } else if (d->cin % 64 == 0) {
+            return f(WG<2, 2, TY, 1, 0, 2>());
+        }
+    }
+    *ok = false;
+    return f(Fam<4>::C11());
+}
+
 template <class F>
 static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
     switch (variant) {
+        case 12:
+        case 13: {
+            bool ok;
+            auto r = variant == 12 ? pick_cw<4>(d, f, &ok) : pick_cw<8>(d, f, &ok);
+            if (ok) return r;
+            break;
+        }
         case 1: return pick_in<Fam<2>>(d, false, f);  // round-1 production: 2-row stages
         case 2: return pick_in<Fam<4>>(d, false, f);  // 4-row stages (C22: 92 KB LDS, 1 block/CU)
         case 3: return pick_in<Fam<4>>(d, true, f);   // 4-row stages, 32-cout tiles (<= 75 KB)
@@ -384,12 +429,19 @@ static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
         case 9: return f(Fam<16, 4>::C11());          // 16-row stages, 4 waves per kernel row
         case 10: return f(Fam<4, 4>::C11());          // 4-row stages, 4 waves per kernel row
         case 11: return f(Fam<16, 2>::C11());         // 16-row stages, 2 waves per kernel row
+        default: break;
+    }
+    switch (0) {
         default:
             if (d->taps == 1) return f(WG<1, 1, 8, 2, 1>());  // stride-2 phase conv: taps {0,1}^2, 4 waves
             // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles; 4-row
             // stages when cin % 64 == 32 (96, 160), else 8-row stages with 2 waves per kernel
             // row (variant 5): 4-11 % under the round-1 choice (16-row stages, 4 waves per
             // row) on cin 64 / 128 / 192 and the sub2 Scaler shape, on two boxes
+            // the RDB final conv (cin 192, cout 64): 64x96 (co, ci) per block, 9 waves splitting the
+            // ci tiles (each pixel tile staged once per block): 81-86 vs 98-104 us
+            if (d->cin == 192 && d->cout == 64 && !d->g_sub2 && !d->x_sub2 && d->ha % 4 == 0)
+                return f(WG<2, 3, 4, 1, 0, 3>());
             if (d->cin % 64 == 32) return f(Fam<4>::C11());
             if (d->ha % 8 == 0) return f(Fam<8, 2>::C11());
             if (d->ha % 4 == 0) return f(Fam<4>::C11());

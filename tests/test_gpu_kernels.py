@@ -291,7 +291,8 @@ def _close_rel(got, ref, tol=2e-2):
 
 @pytest.mark.parametrize("n,cin,cout,h,w,splits", [(2, 64, 32, 20, 36, 0), (1, 96, 32, 33, 65, 0),
                                                    (2, 192, 64, 18, 40, 0), (1, 64, 64, 7, 5, 3),
-                                                   (2, 32, 160, 16, 32, 0), (1, 64, 192, 24, 24, 1)])
+                                                   (2, 32, 160, 16, 32, 0), (1, 64, 192, 24, 24, 1),
+                                                   (1, 192, 64, 20, 36, 5), (1, 160, 32, 9, 70, 0)])
 def test_wgrad3x3(n, cin, cout, h, w, splits):
     from image_super_resolution_amd import ops
     x = bf(_mk(n, cin, h, w, 51))

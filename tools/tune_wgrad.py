@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--variants", default="1,2,3,4")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--splits", default="", help="variant:splits pairs, e.g. 0:128,0:256 (split-K override)")
     args = ap.parse_args()
     lib = _lib.load()
     dev = "cuda"
@@ -31,6 +32,8 @@ def main():
     shapes = [(64, 32, False), (96, 32, False), (128, 32, False), (160, 32, False), (192, 64, False),
               (64, 64, False), (64, 256, True)]
     vs = [int(v) for v in args.variants.split(",")]
+    # (variant, splits) configurations: splits 0 = the library's own choice
+    cfgs = [(v, 0) for v in vs] + [tuple(int(q) for q in c.split(":")) for c in args.splits.split(",") if c]
     for cin, cout, sub2 in shapes:
         g = torch.Generator().manual_seed(cin + cout)
         x = ops.ActBuffer.alloc(n, s, s, 192, 1, dev)
@@ -46,22 +49,24 @@ def main():
         d = ops.wgrad3x3_desc(x, cin, gb, cout, dw, db, g_sub2=sub2)
         st = ops._stream()
         res, ok = {}, []
-        for v in vs:
+        for v, sp in cfgs:
+            d.splits = sp
             nb = lib.isr_wgrad3x3_variant_workspace_bytes(ctypes.byref(d), v)
             ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
             rc = lib.isr_wgrad3x3_variant(ctypes.byref(d), v, ws.data_ptr(), ws.numel(), st)
             if rc == 0:
                 torch.cuda.synchronize()
-                res[v] = (dw.clone(), db.clone(), ws)
-                ok.append(v)
+                res[(v, sp)] = (dw.clone(), db.clone(), ws)
+                ok.append((v, sp))
         times = {v: [] for v in ok}
         for _ in range(args.rounds):
             for v in ok:
                 ws = res[v][2]
+                d.splits = v[1]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(args.reps):
-                    lib.isr_wgrad3x3_variant(ctypes.byref(d), v, ws.data_ptr(), ws.numel(), st)
+                    lib.isr_wgrad3x3_variant(ctypes.byref(d), v[0], ws.data_ptr(), ws.numel(), st)
                 e1.record()
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) / args.reps * 1e3)
@@ -70,9 +75,10 @@ def main():
         base = res[ok[0]][0]
         for v in ok:
             us = statistics.median(times[v])
-            row[f"v{v}_us"] = round(us, 1)
-            row[f"v{v}_tf"] = round(flops / us / 1e6, 0)
-            row[f"v{v}_rel"] = float(((res[v][0] - base).norm() / base.norm()).item())
+            tag = f"v{v[0]}" + (f"s{v[1]}" if v[1] else "")
+            row[f"{tag}_us"] = round(us, 1)
+            row[f"{tag}_tf"] = round(flops / us / 1e6, 0)
+            row[f"{tag}_rel"] = float(((res[v][0] - base).norm() / base.norm()).item())
         print(json.dumps(row), flush=True)
 
 
