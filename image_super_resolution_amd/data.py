@@ -70,7 +70,14 @@ class GPUTransform:
     """Batched (hr, lr) from uint8 HR crops on the device:
     lr = Normalize(Resize(crop, T/scale)) (albumentations Resize = cv2 INTER_LINEAR,
     utils/datasets.py:302-303); hr = 2*crop/255 - 1 (PIL_to_tanh) or
-    Normalize(crop) when hr_norm (set_transform_hr, SRGAN mode)."""
+    Normalize(crop) when hr_norm (set_transform_hr, SRGAN mode).
+
+    cv2 resizes the uint8 image and returns uint8: at the integer factors train.py uses
+    (2, 3, 4) its fixed-point INTER_LINEAR (11-bit coefficients; x2 runs as INTER_AREA)
+    samples at src = scale*(d + 0.5) - 0.5 with weights 0 / 0.5 / 1, i.e. the exact float
+    bilinear value rounded half up — reproduced here by rounding the float interpolation
+    of the uint8 values (oracle.ref_cpu.cv2_resize_linear_u8 restates the fixed-point
+    arithmetic; tests/test_data_cpu.py)."""
 
     def __init__(self, scale: int, hr_norm: bool = False, mean=IMAGENET_MEAN, std=IMAGENET_STD, device="cuda"):
         self.scale, self.hr_norm = scale, hr_norm
@@ -79,11 +86,13 @@ class GPUTransform:
         self.device = device
 
     def __call__(self, crops_u8: torch.Tensor):
-        x = crops_u8.to(self.device, non_blocking=True).float().div_(255.0)
-        t = x.shape[-1]
-        lr = F.interpolate(x, size=(t // self.scale, t // self.scale), mode="bilinear", align_corners=False,
+        x255 = crops_u8.to(self.device, non_blocking=True).float()
+        t = x255.shape[-1]
+        lr = F.interpolate(x255, size=(t // self.scale, t // self.scale), mode="bilinear", align_corners=False,
                            antialias=False)
+        lr = (lr + 0.5).floor_().div_(255.0)  # cv2's uint8 result (round half up), then /255
         lr = (lr - self.mean) / self.std
+        x = x255.div_(255.0)
         hr = (x - self.mean) / self.std if self.hr_norm else x * 2.0 - 1.0
         return hr.contiguous(), lr.contiguous()
 

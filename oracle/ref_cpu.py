@@ -294,3 +294,27 @@ def adv_loss(sr_disc: torch.Tensor, hr_disc: torch.Tensor):
 def ema_decay(updates: int, tau: float, decay: float = 0.9999) -> float:
     """ModelEMA.decay (utils/models.py:27)."""
     return decay * (1 - math.exp(-updates / tau))
+
+
+# ------------------------------------------------------------------ data (LR)
+def cv2_resize_linear_u8(img, scale: int):
+    """SR_dataset's LR resize (utils/datasets.py:302-303: albumentations.Resize, whose default
+    interpolation is cv2.INTER_LINEAR) of a uint8 [..., H, W] array by an integer factor.
+    Third-party: albumentations / OpenCV, absent here and unpinned in the reference
+    (no requirements file) — restated from OpenCV's uint8 resize: destination pixel d samples
+    src = scale*(d + 0.5) - 0.5 with 11-bit fixed-point weights (INTER_RESIZE_COEF_SCALE 2048)
+    and rounds the 22-bit product half up; a x2 downscale runs as INTER_AREA (2x2 mean, also
+    rounded half up).  At integer factors the weights are 0 / 0.5 / 1, so an even factor
+    averages the centre 2x2 of each block, an odd one picks its centre pixel.  Parity
+    unpinned (no cv2 to generate golden vectors)."""
+    import numpy as np
+    a = np.asarray(img).astype(np.int64)
+    H, W = a.shape[-2], a.shape[-1]
+    h, w = H // scale, W // scale
+    if scale % 2:
+        c = (scale - 1) // 2
+        return a[..., c::scale, c::scale][..., :h, :w].astype(np.uint8)
+    c = scale // 2 - 1
+    s = (a[..., c::scale, c::scale][..., :h, :w] + a[..., c + 1::scale, c::scale][..., :h, :w]
+         + a[..., c::scale, c + 1::scale][..., :h, :w] + a[..., c + 1::scale, c + 1::scale][..., :h, :w])
+    return ((s * (1 << 20) + (1 << 21)) >> 22).astype(np.uint8)

@@ -38,3 +38,26 @@ def test_gpu_transform_shapes_cpu():
     hr, lr = t(torch.randint(0, 256, (2, 3, 32, 32), dtype=torch.uint8))
     assert hr.shape == (2, 3, 32, 32) and lr.shape == (2, 3, 16, 16)
     assert float(hr.min()) >= -1 and float(hr.max()) <= 1
+
+
+def test_gpu_transform_lr_matches_cv2_linear_u8():
+    """LR = Normalize(uint8 cv2 INTER_LINEAR resize) of SR_dataset (utils/datasets.py:302-304):
+    GPUTransform (run on the CPU device) vs the oracle's restatement of OpenCV's fixed-point
+    uint8 resize at the integer factors train.py uses; HR = PIL_to_tanh (:96-106) or
+    Normalize (set_transform_hr, :336-339).  cv2 itself is absent: parity unpinned."""
+    import numpy as np
+    from oracle import ref_cpu
+    g = torch.Generator().manual_seed(7)
+    crops = torch.randint(0, 256, (3, 3, 48, 48), generator=g, dtype=torch.uint8)
+    mean = np.array(data.IMAGENET_MEAN, dtype=np.float32).reshape(1, 3, 1, 1)
+    std = np.array(data.IMAGENET_STD, dtype=np.float32).reshape(1, 3, 1, 1)
+    for scale in (2, 3, 4):
+        for hr_norm in (False, True):
+            hr, lr = data.GPUTransform(scale, hr_norm=hr_norm, device="cpu")(crops)
+            lr_u8 = ref_cpu.cv2_resize_linear_u8(crops.numpy(), scale)
+            ref_lr = (lr_u8.astype(np.float32) - mean * 255.0) * (1.0 / (std * 255.0))  # albumentations Normalize
+            assert lr.shape == (3, 3, 48 // scale, 48 // scale)
+            np.testing.assert_allclose(lr.numpy(), ref_lr, rtol=0, atol=2e-6)
+            x = crops.numpy().astype(np.float32)
+            ref_hr = (x / 255.0 - mean) / std if hr_norm else 2.0 * (x / 255.0) - 1.0
+            np.testing.assert_allclose(hr.numpy(), ref_hr, rtol=0, atol=2e-6)
