@@ -956,7 +956,10 @@ int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) {
 // (PixelShuffle order, see isr_conv_desc.x_sub2).
 __device__ __forceinline__ void pack3x3_range(const float* __restrict__ w, __bf16* __restrict__ out, int pcout,
                                               int pcin, int transposed, int sub2, float scale, size_t first,
-                                              size_t stride) {
+                                              size_t stride, int src_n0 = 0, int src_cin = 0) {
+    // dgrad window: packed output channel n = layer input channel src_n0 + n of a layer with
+    // src_cin input channels (row stride of w); 0 → the whole layer (src_cin = pcout)
+    const int wrow = src_cin > 0 ? src_cin : pcout;
     const size_t total = (size_t)pcout * pcin * 9;
     for (size_t idx = first; idx < total; idx += stride) {
         size_t rem = idx;
@@ -973,7 +976,7 @@ __device__ __forceinline__ void pack3x3_range(const float* __restrict__ w, __bf1
         } else {
             const int cs4 = pcin >> 2;
             const int co = sub2 ? (ci % cs4) * 4 + ci / cs4 : ci;  // layer output channel
-            v = w[((size_t)co * pcout + n) * 9 + (8 - tap)];       // layer W[co][n][8 - tap]; layer cin = pcout
+            v = w[((size_t)co * wrow + src_n0 + n) * 9 + (8 - tap)];  // layer W[co][n0 + n][8 - tap]
         }
         out[idx] = (__bf16)(v * scale);
     }
@@ -991,7 +994,8 @@ __global__ void pack3x3_batch_kernel(const isr_pack_item* __restrict__ items) {
     const isr_pack_item it = items[blockIdx.y];
     const int pcout = it.dgrad ? it.cin : it.cout, pcin = it.dgrad ? it.cout : it.cin;
     pack3x3_range(it.w, (__bf16*)it.out, pcout, pcin, it.dgrad, it.sub2, it.dgrad ? it.scale : 1.f,
-                  blockIdx.x * (size_t)blockDim.x + threadIdx.x, (size_t)gridDim.x * blockDim.x);
+                  blockIdx.x * (size_t)blockDim.x + threadIdx.x, (size_t)gridDim.x * blockDim.x,
+                  it.dgrad ? it.src_n0 : 0, it.dgrad ? it.src_cin : 0);
 }
 
 int conv3x3_pack_batch(const isr_pack_item* items, int n, hipStream_t s) {

@@ -153,19 +153,28 @@ def pack_conv3x3_dgrad(w: torch.Tensor, scale: float = 1.0, sub2: bool = False,
 
 def pack_batch_table(items, device) -> tuple[torch.Tensor, int]:
     """Device table of isr_pack_item for isr_pack_conv3x3_batch.  items: tuples
-    (w fp32 [cout,cin,3,3], out packed bf16, cout, cin, dgrad, sub2, scale); the
-    tensors must stay alive and in place (parameters, packed buffers)."""
+    (w fp32 [cout,cin,3,3], out packed bf16, cout, cin, dgrad, sub2, scale) or, for a
+    dgrad window (isr.h isr_pack_item), (w [cout,src_cin,3,3], out, cout, cin, 1, 0, scale,
+    src_n0, src_cin, out_elem_offset) with out_elem_offset the block's bf16 element offset
+    inside `out`; the tensors must stay alive and in place (parameters, packed buffers)."""
     import struct
     raw = bytearray()
-    for w, out, cout, cin, dgrad, sub2, scale in items:
+    lib = _lib.load()
+    for it in items:
+        w, out, cout, cin, dgrad, sub2, scale = it[:7]
+        n0, scin, eoff = (it[7], it[8], it[9]) if len(it) > 7 else (0, 0, 0)
         _require_gpu(w, "pack_conv3x3_batch")
-        if w.dtype != torch.float32 or not w.is_contiguous() or tuple(w.shape) != (cout, cin, 3, 3):
-            raise ValueError("pack_conv3x3_batch: weights must be contiguous fp32 [cout, cin, 3, 3]")
+        wshape = (cout, scin if scin else cin, 3, 3)
+        if w.dtype != torch.float32 or not w.is_contiguous() or tuple(w.shape) != wshape:
+            raise ValueError(f"pack_conv3x3_batch: weights must be contiguous fp32 {list(wshape)}")
         if cin % 16 or cout % 32 or (dgrad and (cin % 32 or cout % 16)):
             raise ValueError(f"pack_conv3x3_batch: unsupported shape cout={cout} cin={cin}")
-        if out.dtype != torch.bfloat16 or out.numel() * 2 < _lib.load().isr_conv3x3_packed_bytes(cout, cin):
+        if scin and (not dgrad or sub2 or n0 < 0 or n0 + cin > scin):
+            raise ValueError("pack_conv3x3_batch: bad dgrad window")
+        if out.dtype != torch.bfloat16 or out.numel() < eoff + lib.isr_conv3x3_packed_bytes(cout, cin) // 2:
             raise ValueError("pack_conv3x3_batch: bad output buffer")
-        raw += struct.pack("<QQiiiifi", w.data_ptr(), out.data_ptr(), cout, cin, int(dgrad), int(sub2), float(scale), 0)
+        raw += struct.pack("<QQiiiifiii", w.data_ptr(), out.data_ptr() + 2 * eoff, cout, cin, int(dgrad), int(sub2),
+                           float(scale), int(n0), int(scin), 0)
     table = torch.frombuffer(raw, dtype=torch.uint8).to(device)
     return table, len(items)
 

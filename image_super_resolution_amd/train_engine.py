@@ -28,6 +28,8 @@ conv's wgrad/dgrad, and dgamma/dbeta land in the flat gradient buffer.
 """
 from __future__ import annotations
 
+import os as _os
+
 import ctypes
 from dataclasses import dataclass
 
@@ -158,6 +160,21 @@ class GeneratorTrainPlan:
                     self._goff.append(off)
                     off += (p.numel() + 3) // 4 * 4  # 16-byte aligned views
         self._gsize = off
+        # RDB input gradients as "gather" convs (no BatchNorm): per RDB, one conv per dense-buffer
+        # block — the gradient of block o_t (and of x) is ONE conv over the concatenated output
+        # gradients of every conv that read it (forward-shaped: K 576..1728, 32 / 64 outputs,
+        # each output written once) instead of an accumulate-into-all-channels transposed conv
+        # per layer (K 288, read-modify-write of 64..192 channels).  Weights: slices of the
+        # layers' transposed weights, packed per step by the same batched launch.
+        self.gather = (not self.has_bn) and _os.environ.get("ISR_TRAIN_GATHER", "1") == "1"
+        if self.gather:
+            nbytes = self.lib.isr_conv3x3_packed_bytes
+            self.gpacks = []
+            for _ in self.rdbs:
+                gp = {t: torch.empty(nbytes(32, 64 + 32 * (3 - t)) // 2, dtype=torch.bfloat16, device=dev)
+                      for t in range(4)}
+                gp["x"] = torch.empty(nbytes(64, 192) // 2, dtype=torch.bfloat16, device=dev)
+                self.gpacks.append(gp)
         self.pack()
         self._build()
 
@@ -172,15 +189,44 @@ class GeneratorTrainPlan:
         if getattr(self, "_pack_items", None) is None:
             for c in self.convs:  # first call: allocate the packed buffers
                 c.pack()
+            rdb_convs = {id(c) for r in self.rdbs for c in r} if self.gather else set()
             self._pack_items = ops.pack_batch_table(
                 [(c.w, c.fwd, c.cout, c.cin, False, False, 1.0) for c in self.convs if c.kind == "3x3"]
-                + [(c.w, c.bwd, c.cout, c.cin, True, c.sub2, c.dgrad_scale) for c in self.convs if c.kind == "3x3"],
+                + [(c.w, c.bwd, c.cout, c.cin, True, c.sub2, c.dgrad_scale) for c in self.convs
+                   if c.kind == "3x3" and id(c) not in rdb_convs]
+                + (self._gather_items() if self.gather else []),
                 self.device)
+            ops.pack_batch(self._pack_items)
             return
         ops.pack_batch(self._pack_items)
         for c in self.convs:
             if c.kind != "3x3":
                 c.pack()
+
+    def _gather_items(self) -> list:
+        """isr_pack_item windows for the RDB input-gradient gather convs (see __init__).
+        Target o_t (t = 3..0): output = the 32 input channels [64+32t, 96+32t) of the RDB's
+        dense buffer; input = [g_f | g_3 | ... | g_{t+1}] (64 + 32 (3-t) channels: the final
+        conv's output gradient, then each growth conv's); target x: output = channels [0, 64),
+        input = all 192.  Block weights = the producing layer's transposed weights restricted
+        to the target's channels; the final conv's block carries its RDB scale a (and the
+        RRDB's a for the third RDB: utils/models.py:265-271, 316-317)."""
+        a, items = self.a, []
+        for j, cs in enumerate(self.rdbs):
+            res = a if j % 3 == 2 else 1.0
+            c5 = cs[4]
+            gp = self.gpacks[j]
+            for t in list(range(3, -1, -1)) + ["x"]:
+                out = gp[t]
+                if t == "x":
+                    n0, co, srcs = 0, 64, list(range(3, -1, -1))
+                else:
+                    n0, co, srcs = 64 + 32 * t, 32, list(range(3, t, -1))
+                items.append((c5.w, out, 64, co, True, False, a * res, n0, 192, 0))
+                for k in srcs:
+                    off = 64 + 32 * (3 - k)  # input-channel offset of g_k in the gather input
+                    items.append((cs[k].w, out, 32, co, True, False, 1.0, n0, cs[k].cin, (off // 16) * 9 * co * 16))
+        return items
 
     def _build(self):
         a, lib = self.a, self.lib
@@ -260,7 +306,26 @@ class GeneratorTrainPlan:
         B.append(("conv", ops.conv3x3_desc(g1, 64, c.bwd, None, 64, U)))
         # RRDBs, reverse
         nb = len(self.rdbs) // 3
-        for i in range(nb - 1, -1, -1):
+        for i in range(nb - 1, -1, -1) if self.gather else ():
+            # gather form (no BN): E (= gin) holds [g_out | g_3 | g_2 | g_1 | g_0]; g_out (the RDB
+            # output gradient) arrives in E[0:64], each target conv appends its block, the x
+            # target writes the RDB input gradient into gout[0:64] (the next E)
+            seq = [(3 * i + 2, U, V), (3 * i + 1, V, W), (3 * i, W, V)]
+            for step, (j, E, gout) in enumerate(seq):
+                cs, Dj, gp = self.rdbs[j], D[j], self.gpacks[j]
+                res = a if step == 0 else 1.0
+                wg3(Dj, 192, E, 64, cs[4], scale=a * res)
+                for t in range(3, -1, -1):
+                    slot = 64 + 32 * (3 - t)
+                    B.append(("conv", ops.conv3x3_desc(E, slot, gp[t], None, 32, E, y_coff=slot, m=Dj,
+                                                       m_coff=64 + 32 * t, m_c0=0, mslope=LEAKY)))
+                    wg3(Dj, cs[t].cin, E, 32, cs[t], g_coff=slot)
+                # v = (acc / res + g_out) * res (+ g_R: the RRDB's own residual, first RDB)
+                kw = dict(r2=U) if step == 2 else {}
+                B.append(("conv", ops.conv3x3_desc(E, 192, gp["x"], None, 64, gout, r1=E, s1=1.0 / res, s2=res,
+                                                   **kw)))
+            U, V, W = V, W, U
+        for i in range(nb - 1, -1, -1) if not self.gather else ():
             # g_R (gradient wrt the RRDB output) is in U[0:64]
             seq = [(3 * i + 2, U, V), (3 * i + 1, V, W), (3 * i, W, V)]
             for step, (j, gin, gout) in enumerate(seq):

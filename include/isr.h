@@ -288,12 +288,19 @@ int isr_pack_conv3x3_dgrad(const float* w_oihw, void* packed, int32_t cout, int3
                            isr_stream_t s);
 /* Many isr_pack_conv3x3 / isr_pack_conv3x3_dgrad in one launch (items: device array). */
 typedef struct isr_pack_item {
-    const float* w; /* layer weights [cout][cin][3][3] fp32 */
+    const float* w; /* layer weights [cout][cin][3][3] fp32 (dgrad with src_cin > 0: [cout][src_cin][3][3]) */
     void* out;      /* packed bf16, isr_conv3x3_packed_bytes(cout, cin) bytes */
     int32_t cout, cin;
     int32_t dgrad;  /* 0: forward pack; 1: dgrad pack (as isr_pack_conv3x3_dgrad) */
     int32_t sub2;
     float scale;
+    /* dgrad window (0, 0 = the whole layer): pack only the layer's input channels
+     * [src_n0, src_n0 + cin) of a layer with src_cin input channels, i.e. the slice of the
+     * transposed conv that produces those channels.  `out` may point inside a larger pack: a
+     * conv whose input concatenates several layers' output gradients (the RDB input-gradient
+     * "gather" convs of the training backward) is packed as one item per input block, at
+     * packed offset (block's first input channel / 16) * 9 * cin * 16 elements. */
+    int32_t src_n0, src_cin;
     int32_t pad_;
 } isr_pack_item;
 int isr_pack_conv3x3_batch(const isr_pack_item* items, int32_t n, isr_stream_t s);

@@ -46,6 +46,7 @@ int main(void) {
   F(isr_head_desc, slope); F(isr_tail_desc, x); F(isr_tail_desc, y); F(isr_tail_desc, y_u8);
   S(isr_chain_desc); F(isr_chain_desc, kinds); F(isr_chain_desc, nl); F(isr_chain_desc, wa);
   F(isr_chain_desc, state); F(isr_chain_desc, acquire);
+  S(isr_pack_item); F(isr_pack_item, scale); F(isr_pack_item, src_n0); F(isr_pack_item, src_cin);
   return 0;
 }
 """
@@ -62,10 +63,13 @@ def test_struct_layouts_match_c(tmp_path):
           "isr_chain_desc": ctypes.sizeof(_lib.IsrChainDesc)}
     for k, v in py.items():
         assert int(c[k]) == v, k
+    # isr_pack_item is written by ops.pack_batch_table with struct "<QQiiiifiii"
+    assert int(c["isr_pack_item"]) == 48
+    assert (int(c["isr_pack_item.scale"]), int(c["isr_pack_item.src_n0"]), int(c["isr_pack_item.src_cin"])) == (32, 36, 40)
     cls = {"isr_view": _lib.IsrView, "isr_conv_desc": _lib.IsrConvDesc, "isr_head_desc": _lib.IsrHeadDesc,
            "isr_tail_desc": _lib.IsrTailDesc, "isr_chain_desc": _lib.IsrChainDesc}
     for key, val in c.items():
-        if "." in key:
+        if "." in key and not key.startswith("isr_pack_item"):
             s, m = key.split(".")
             assert getattr(cls[s], m).offset == int(val), key
 
