@@ -246,6 +246,7 @@ class GeneratorTrainPlan:
                 F.append(("bnf", ops.bn_desc(z, y, c.cout, c.bn_state, c.bn, z_coff=z_coff, y_coff=y_coff,
                                              slope=slope, **res), c.bn_state))
 
+        trunk0 = len(F)
         for j, cs in enumerate(self.rdbs):
             Zj = self.Zb[j] if self.has_bn else None
             for k in range(4):
@@ -254,6 +255,18 @@ class GeneratorTrainPlan:
             c = cs[4]
             extra = dict(r2=D[j - 2], s2=a) if j % 3 == 2 else {}
             conv_bn(D[j], 192, c, D[j + 1], 0, Zj, 0, 1.0, r1=D[j], s1=a, **extra)
+        self.chain = None
+        if not self.has_bn and self.rdbs and _os.environ.get("ISR_TRAIN_CHAIN", "1") == "1":
+            # no BatchNorm: the whole trunk forward as ONE persistent isr_conv_chain launch (as
+            # inference, engine.ConvChain); every RDB writes its own dense buffer here
+            from .engine import ConvChain
+            try:
+                from .engine import CHAIN_ACQUIRE
+                self.chain = ConvChain([e[1] for e in F[trunk0:]], D[0], self.device, acquire=CHAIN_ACQUIRE)
+            except ValueError:
+                self.chain = None
+            if self.chain is not None:
+                F[trunk0:] = [(self.chain.fn, self.chain.desc)]
         c = self.conv1
         conv_bn(D[-1], 64, c, T, 0, self.Tz if self.has_bn else None, 0, 1.0, r1=f0, s1=1.0)
         cur = T
