@@ -284,6 +284,44 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
 }
 
 // dW[co][ci][tap] (reference OIHW) = scale * sum_s ws[s][tap][co'][ci];  co' = kernel channel order.
+// One block per (co', 32-ci run): 4 split-slices x 32 ci threads each sum 9 tap rows
+// (coalesced 128-B reads per tap), the slices are added through LDS, and the block writes its
+// 32 x 9 outputs as ONE contiguous run of dW — the transposing scatter of the column-wise
+// reduce below (4-B stores 36 B apart) took 0.5 ms per call on the discriminator's 512 x 2048
+// phase-expanded weight.  Requires cin % 32 == 0.
+__global__ __launch_bounds__(128) void wgrad_reduce_t_kernel(WgradArgs a) {
+    __shared__ float red[4][9][33];
+    const isr_wgrad_desc& d = a.d;
+    const size_t per = (size_t)9 * d.cout * d.cin;
+    const size_t row = per + d.cout;
+    const int ncb = d.cin / 32;
+    const int cok = blockIdx.x / ncb, ci0 = (blockIdx.x - cok * ncb) * 32;
+    const int c = threadIdx.x & 31, slice = threadIdx.x >> 5;
+    float acc[9], bacc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = 0.f;
+    const float* src = a.ws + (size_t)cok * d.cin + ci0 + c;
+    const bool bias_blk = d.db && ci0 == 0;
+    for (int sp = slice; sp < a.splits; sp += 4) {
+        const float* r = src + (size_t)sp * row;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t] += r[(size_t)t * d.cout * d.cin];
+        if (bias_blk && c == 0) bacc += a.ws[(size_t)sp * row + per + cok];
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) red[slice][t][c] = acc[t];
+    if (bias_blk && c == 0) red[slice][0][32] = bacc;
+    __syncthreads();
+    const int cs4 = d.cout >> 2;
+    const int co = d.g_sub2 ? (cok % cs4) * 4 + cok / cs4 : cok;
+    float* dst = d.dw + ((size_t)co * d.cin + ci0) * 9;
+    for (int o = threadIdx.x; o < 32 * 9; o += 128) {
+        const int cc = o / 9, t = o - cc * 9;
+        dst[o] = (red[0][t][cc] + red[1][t][cc] + red[2][t][cc] + red[3][t][cc]) * d.scale;
+    }
+    if (bias_blk && threadIdx.x == 0) d.db[co] = (red[0][0][32] + red[1][0][32] + red[2][0][32] + red[3][0][32]) * d.scale;
+}
+
 // Workspace rows are [splits][9*cout*cin + cout] (the bias partials follow each
 // split's dW partials).  Block = 4 split-slices x 64 float4 columns: every
 // thread streams S/4 rows of one 16-byte column (independent loads in flight),
@@ -354,7 +392,10 @@ static void wgrad_geometry(const isr_wgrad_desc* d, int* tiles, int* splits) {
     // earlier ~640-block target, whose extra partials cost more in the reduce than they gain
     const int target = C::CW > 1 ? (C::LDS > 81920 ? 512 : 1024) / (C::CO_T == 64 && d->cin > C::CI_T ? 2 : 1)
                                  : (C::KW > 2 ? 640 * 2 / C::KW : (C::KW == 2 ? 512 : 640));
-    *splits = wgrad_splits(d, *tiles, (d->cout / C::CO_T) * (d->cin / C::CI_T), target, C::KW == 2 ? 64 : 1);
+    // (the 64-split floor only for the generator's few-pair shapes: the discriminator's wide
+    // layers have 64..1024 pairs, where it would multiply the partials — 2.4 GB at 512 x 2048)
+    const int pairs = (d->cout / C::CO_T) * (d->cin / C::CI_T);
+    *splits = wgrad_splits(d, *tiles, pairs, target, C::KW == 2 && pairs <= 16 ? 64 : 1);
 }
 
 template <class C>
@@ -370,6 +411,13 @@ static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipS
     const int blocks = a.splits * (d->cout / C::CO_T) * (d->cin / C::CI_T);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, a);
     if (hipGetLastError() != hipSuccess) return -1;
+    // the transposing reduce has one block per (co, 32 ci): it pays only for large weights (the
+    // discriminator's phase-expanded 128..512 x 512..2048); the generator's <= 256 x 192 keep
+    // the column-wise reduce (more blocks: 30 vs 48 us per wgrad at 32 x 64)
+    if (d->cin % 32 == 0 && (size_t)d->cout * d->cin >= 65536) {
+        hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)(d->cout * (d->cin / 32))), dim3(128), 0, s, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     const size_t nv = ((size_t)9 * d->cout * d->cin + d->cout) / 4;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nv + 63) / 64)), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
