@@ -283,10 +283,10 @@ class GeneratorTrainPlan:
         ci = {id(c): i for i, c in enumerate(self.convs)}
         dev = self.device
 
-        def wg3(x, cin, g, cout, c, *, x_coff=0, g_coff=0, scale=1.0, g_sub2=False):
+        def wg3(x, cin, g, cout, c, *, x_coff=0, g_coff=0, scale=1.0, g_sub2=False, side=False):
             d = ops.wgrad3x3_desc(x, cin, g, cout, _meta_dw(cout, cin, 3, dev), None, x_coff=x_coff, g_coff=g_coff,
                                   scale=scale, g_sub2=g_sub2)
-            B.append(("wg3", d, ci[id(c)]))
+            B.append(("wg3", d, ci[id(c)], side))
 
         # tail
         self.gp = torch.empty(self.out_shape, device=dev)
@@ -319,25 +319,37 @@ class GeneratorTrainPlan:
         B.append(("conv", ops.conv3x3_desc(g1, 64, c.bwd, None, 64, U)))
         # RRDBs, reverse
         nb = len(self.rdbs) // 3
-        for i in range(nb - 1, -1, -1) if self.gather else ():
-            # gather form (no BN): E (= gin) holds [g_out | g_3 | g_2 | g_1 | g_0]; g_out (the RDB
-            # output gradient) arrives in E[0:64], each target conv appends its block, the x
-            # target writes the RDB input gradient into gout[0:64] (the next E)
-            seq = [(3 * i + 2, U, V), (3 * i + 1, V, W), (3 * i, W, V)]
-            for step, (j, E, gout) in enumerate(seq):
-                cs, Dj, gp = self.rdbs[j], D[j], self.gpacks[j]
-                res = a if step == 0 else 1.0
-                wg3(Dj, 192, E, 64, cs[4], scale=a * res)
-                for t in range(3, -1, -1):
-                    slot = 64 + 32 * (3 - t)
-                    B.append(("conv", ops.conv3x3_desc(E, slot, gp[t], None, 32, E, y_coff=slot, m=Dj,
-                                                       m_coff=64 + 32 * t, m_c0=0, mslope=LEAKY)))
-                    wg3(Dj, cs[t].cin, E, 32, cs[t], g_coff=slot)
-                # v = (acc / res + g_out) * res (+ g_R: the RRDB's own residual, first RDB)
-                kw = dict(r2=U) if step == 2 else {}
-                B.append(("conv", ops.conv3x3_desc(E, 192, gp["x"], None, 64, gout, r1=E, s1=1.0 / res, s2=res,
-                                                   **kw)))
-            U, V, W = V, W, U
+        if self.gather:
+            # gather form (no BN): one gradient dense buffer per RDB, E_j = [g_out | g_3 | g_2 |
+            # g_1 | g_0]; g_out (the RDB output gradient) arrives in E_j[0:64], each target conv
+            # appends its block, the x target writes the RDB input gradient into E_{j-1}[0:64]
+            # (RDB 0: into `self.gtrunk`).  Nothing is overwritten, so the five weight gradients
+            # of RDB j run on a second HIP stream (`side`) as soon as its target 0 is done
+            # ("evrec" / "evwait"), beside the next RDBs' gather convs.
+            nr = len(self.rdbs)
+            self.Eg = [ActBuffer.alloc(n_, h_, w_, 192, 1, dev) for n_, h_, w_ in [(D[0].n, D[0].h, D[0].w)] * nr]
+            self.gtrunk = ActBuffer.alloc(D[0].n, D[0].h, D[0].w, 64, 1, dev)
+            # conv1's input gradient (g_R of the last RRDB) goes straight into E_{nr-1}[0:64]
+            B[-1] = ("conv", ops.conv3x3_desc(g1, 64, c.bwd, None, 64, self.Eg[nr - 1]))
+            for i in range(nb - 1, -1, -1):
+                for step, j in enumerate((3 * i + 2, 3 * i + 1, 3 * i)):
+                    cs, Dj, gp, E = self.rdbs[j], D[j], self.gpacks[j], self.Eg[j]
+                    gout = self.Eg[j - 1] if j > 0 else self.gtrunk
+                    res = a if step == 0 else 1.0
+                    for t in range(3, -1, -1):
+                        slot = 64 + 32 * (3 - t)
+                        B.append(("conv", ops.conv3x3_desc(E, slot, gp[t], None, 32, E, y_coff=slot, m=Dj,
+                                                           m_coff=64 + 32 * t, m_c0=0, mslope=LEAKY)))
+                    B.append(("evrec", j))
+                    B.append(("evwait", j))
+                    wg3(Dj, 192, E, 64, cs[4], scale=a * res, side=True)
+                    for t in range(3, -1, -1):
+                        wg3(Dj, cs[t].cin, E, 32, cs[t], g_coff=64 + 32 * (3 - t), side=True)
+                    # v = (acc / res + g_out) * res (+ g_R: the RRDB's own residual, first RDB)
+                    kw = dict(r2=self.Eg[3 * i + 2]) if step == 2 else {}
+                    B.append(("conv", ops.conv3x3_desc(E, 192, gp["x"], None, 64, gout, r1=E, s1=1.0 / res, s2=res,
+                                                       **kw)))
+            U = self.gtrunk
         for i in range(nb - 1, -1, -1) if not self.gather else ():
             # g_R (gradient wrt the RRDB output) is in U[0:64]
             seq = [(3 * i + 2, U, V), (3 * i + 1, V, W), (3 * i, W, V)]
@@ -389,6 +401,12 @@ class GeneratorTrainPlan:
             raise RuntimeError("train plan: could not size the wgrad workspace: "
                                + lib.isr_last_error().decode(errors="replace"))
         self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        # the side stream's weight gradients get a workspace of their own (they run concurrently
+        # with the main stream's)
+        self.ws_side = torch.empty(nbytes, dtype=torch.uint8, device=dev) if self.gather else None
+        self.side = (torch.cuda.Stream(dev) if self.gather and _os.environ.get("ISR_TRAIN_SIDE", "1") == "1"
+                     else None)
+        self.events = {}
         # gradient offsets per conv: (w, b or None, bn weight or None, bn bias or None)
         self._conv_goff = []
         pi = 0
@@ -443,8 +461,25 @@ class GeneratorTrainPlan:
         gbase = grads.data_ptr()
         lib, st, byref = self.lib, ops._stream(), ctypes.byref
         ws, wsn = self.ws.data_ptr(), self.ws.numel()
+        main = torch.cuda.current_stream(self.device)
+        side_used = False
+        if self.side is not None:
+            self.side.wait_stream(main)  # `grads` and the forward's activations are ready
+            sst = ctypes.c_void_p(self.side.cuda_stream)
         for e in self.bwd_launches:
             kind, d = e[0], e[1]
+            if kind in ("evrec", "evwait") and self.side is None:
+                continue
+            if kind == "evrec":
+                ev = self.events.get(d)
+                if ev is None:
+                    ev = self.events[d] = torch.cuda.Event()
+                ev.record(main)
+                continue
+            if kind == "evwait":
+                self.side.wait_event(self.events[d])
+                side_used = True
+                continue
             if kind == "conv":
                 rc = lib.isr_conv3x3_fwd(byref(d), st)
             elif kind == "bnb":
@@ -458,13 +493,18 @@ class GeneratorTrainPlan:
                 wo, bo = self._conv_goff[e[2]][:2]
                 d.dw = gbase + 4 * wo
                 d.db = gbase + 4 * bo if bo is not None else None
-                rc = (lib.isr_wgrad3x3 if kind == "wg3" else lib.isr_wgrad9x9)(byref(d), ws, wsn, st)
+                if kind == "wg3" and e[3] and self.side is not None:
+                    rc = lib.isr_wgrad3x3(byref(d), self.ws_side.data_ptr(), self.ws_side.numel(), sst)
+                else:
+                    rc = (lib.isr_wgrad3x3 if kind == "wg3" else lib.isr_wgrad9x9)(byref(d), ws, wsn, st)
             elif kind == "head":
                 rc = lib.isr_head9x9_fwd(byref(d), st)
             else:
                 rc = lib.isr_ew_combine(byref(d), st)
             if rc != 0:
                 ops.check(rc, f"train backward ({kind})")
+        if side_used:
+            main.wait_stream(self.side)
         group = self.gen.__dict__.get("_isr_grad_group")
         if group is not None:
             # data-parallel: one RCCL all-reduce of the whole flat gradient buffer
