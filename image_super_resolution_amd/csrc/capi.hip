@@ -467,8 +467,9 @@ int isr_maxpool2_bwd(const isr_pool_desc* d, isr_stream_t s) {
 
 static int bn_validate(const isr_bn_desc* d, int op) {
     if (!d) return fail(ISR_ERR_BAD_DESC, "bn: null descriptor");
-    if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0 || d->c % 16)
-        return fail(ISR_ERR_BAD_DESC, "bn: bad problem n=%d h=%d w=%d c=%d", d->n, d->h, d->w, d->c);
+    if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0 || d->c % 16 || d->c > 1024)
+        return fail(ISR_ERR_BAD_DESC, "bn: bad problem n=%d h=%d w=%d c=%d (c %% 16 == 0, c <= 1024)", d->n, d->h,
+                    d->w, d->c);
     if (d->ha < d->h || d->wa < d->w) return fail(ISR_ERR_BAD_DESC, "bn: computed region smaller than valid");
     if (!d->acc || !d->save) return fail(ISR_ERR_BAD_DESC, "bn: null acc / save");
     if (op != 1 && !view_ok(d->z, d->ha, d->wa, 0, d->c, "bn.z", 1)) return ISR_ERR_BAD_DESC;

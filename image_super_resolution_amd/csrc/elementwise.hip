@@ -393,7 +393,17 @@ __global__ void bn_finalize_kernel(isr_bn_desc d) {
 
 // y = ((act(a*z + b)) * s1 + r1) * s2 + r2;  a = gamma*invstd, b = beta - mean*a
 template <typename I>
+#define BN_MAX_C 1024  // channels per BatchNorm layer (validated on the host)
+
 __global__ __launch_bounds__(256) void bn_apply_kernel(isr_bn_desc d) {
+    // per-channel affine (a, b) once per block in LDS: the element loop is one FMA per value
+    __shared__ float ca[BN_MAX_C], cb[BN_MAX_C];
+    for (int c = threadIdx.x; c < d.c; c += blockDim.x) {
+        const float a = d.gamma[c] * d.save[d.c + c];
+        ca[c] = a;
+        cb[c] = d.beta[c] - d.save[c] * a;
+    }
+    __syncthreads();
     const int cg = d.c / 8;
     const I total = (I)((size_t)d.n * d.ha * d.wa * cg);
     for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
@@ -409,9 +419,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(isr_bn_desc d) {
             load8_bf16(view_at(d.z, img, y, x, c), v);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const float a = d.gamma[c + k] * d.save[d.c + c + k];
-                const float bb = d.beta[c + k] - d.save[c + k] * a;
-                float t = v[k] * a + bb;
+                float t = v[k] * ca[c + k] + cb[c + k];
                 t = t >= 0.f ? t : t * d.slope;
                 v[k] = t * d.s1;
             }
@@ -437,9 +445,21 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(isr_bn_desc d) {
 // dz = gscale * a * (g - sum(g)/N - xhat * sum(g*xhat)/N), in place over y; dgamma/dbeta
 template <typename I>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(isr_bn_desc d) {
+    // dz = gs*gamma*istd * (g - mean(g) - xhat * mean(g*xhat)) = A*g + B*z + C per channel, with
+    // A, B, C computed once per block in LDS (the element loop had two fp64 divides per value)
+    __shared__ float ca[BN_MAX_C], cb[BN_MAX_C], cc[BN_MAX_C];
     const int cg = d.c / 8;
     const I total = (I)((size_t)d.n * d.ha * d.wa * cg);
     const double cnt = (double)d.n * d.h * d.w;
+    for (int c = threadIdx.x; c < d.c; c += blockDim.x) {
+        const float mean = d.save[c], istd = d.save[d.c + c];
+        const float mg = (float)(d.acc[c] / cnt), mgx = (float)(d.acc[d.c + c] / cnt);
+        const float A = d.gscale * d.gamma[c] * istd;
+        ca[c] = A;
+        cb[c] = -A * istd * mgx;
+        cc[c] = A * (mean * istd * mgx - mg);
+    }
+    __syncthreads();
     if (blockIdx.x == 0) {
         for (int c = threadIdx.x; c < d.c; c += blockDim.x) {
             if (d.dgamma) d.dgamma[c] = (float)(d.acc[d.c + c]) * d.gscale;
@@ -460,12 +480,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(isr_bn_desc d) {
             load8_bf16(view_at(d.z, img, y, x, c), z);
             load8_bf16(view_at(d.y, img, y, x, c), g);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const float mean = d.save[c + k], istd = d.save[d.c + c + k];
-                const float mg = (float)(d.acc[c + k] / cnt), mgx = (float)(d.acc[d.c + c + k] / cnt);
-                const float xh = (z[k] - mean) * istd;
-                v[k] = d.gscale * d.gamma[c + k] * istd * (g[k] - mg - xh * mgx);
-            }
+            for (int k = 0; k < 8; ++k) v[k] = ca[c + k] * g[k] + (cb[c + k] * z[k] + cc[c + k]);
         }
         store8_bf16(view_at(d.dz.data ? d.dz : d.y, img, y, x, c), v);
     }

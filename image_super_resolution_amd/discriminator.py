@@ -154,6 +154,12 @@ class DiscriminatorPlan:
         return out
 
     def pack(self) -> None:
+        # repack only when a weight changed since this plan's last pack (an SRGAN step runs three
+        # forwards on the same weights); HIP optimiser writes bump ops.param_write_epoch
+        key = (ops.param_write_epoch(),) + tuple((l.w.data_ptr(), l.w._version) for l in self.layers)
+        if key == getattr(self, "_pack_key", None):
+            return
+        self._pack_key = key
         for l in self.layers:
             w = l.w.detach().float()
             if l.cin_p != l.cin:
