@@ -22,6 +22,7 @@ statistics in double (isr_bn_*).
 from __future__ import annotations
 
 import ctypes
+import os as _os
 
 import torch
 from torch import nn
@@ -75,6 +76,10 @@ def gather_wgrad(dwp: torch.Tensor, ci: int) -> torch.Tensor:
             s = 2 * a + b
             dw[:, :, dy, dx] = dwp[:, s * ci:(s + 1) * ci, ty, tx]
     return dw
+
+
+# ISR_DISC_REUSE=0: always recompute (A/B)
+REUSE = _os.environ.get("ISR_DISC_REUSE", "1") == "1"
 
 
 class _Layer:
@@ -173,8 +178,33 @@ class DiscriminatorPlan:
                 l.bwd = ops.pack_conv3x3_dgrad(wb, out=l.bwd)
 
     # ----------------------------------------------------------------- forward
+    def _input_key(self, x: torch.Tensor):
+        """Identity of this forward's input and weights: the same storage (held by the plan, so
+        its address cannot be reused meanwhile), view, version counter and the same parameter
+        versions (torch optimisers bump _version; the HIP optimisers bump `_isr_wv`)."""
+        return ((x.untyped_storage().data_ptr(), x.storage_offset(), tuple(x.shape), x.stride(), x._version,
+                 x.dtype)
+                + tuple((p.data_ptr(), p._version, p.__dict__.get("_isr_wv", 0)) for p in self.params()))
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        """x [n, 3, h, w] fp32 → conv-stack features [n, C, h/16, w/16] fp32 (BN in train mode)."""
+        """x [n, 3, h, w] fp32 → conv-stack features [n, C, h/16, w/16] fp32 (BN in train mode).
+
+        A forward of the same input with unchanged weights right after this plan's previous one
+        (SRGAN: the discriminator step's D(sr.detach()) repeats the generator step's D(sr),
+        train.py:104 / :126, with D not yet updated) reuses the stored activations: only the
+        BatchNorm running-statistics update of each layer is replayed, from the forward's own
+        batch sums (bit-identical to recomputing)."""
+        key = self._input_key(x) if REUSE else None
+        if key is not None and key == getattr(self, "_fwd_key", None):
+            for l, d in zip(self.layers, self._bn_descs):
+                if l.bn is not None:
+                    l.bn_state.acc.copy_(l.fwd_acc)
+                    ops.check(ops._lib.load().isr_bn_finalize(ctypes.byref(d), ops._stream()), "isr_bn_finalize")
+                    if l.bn.num_batches_tracked is not None:
+                        l.bn.num_batches_tracked.add_(1)
+            return ops.blocked_to_nchw(self.A[-1], torch.empty(self.feat_shape, device=self.device))
+        self._fwd_key, self._fwd_x = key, (x.untyped_storage() if key is not None else None)
+        self._bn_descs = []
         ops.nchw_to_blocked(x.float().contiguous(), self.xin)
         prev = self.xin
         for i, l in enumerate(self.layers):
@@ -185,10 +215,17 @@ class DiscriminatorPlan:
                             x_sub2=True, taps=1)
             else:
                 ops.conv3x3(prev, l.cin_p, l.fwd, bias, l.cout, y, slope=1.0 if l.bn is not None else SLOPE)
+            d = None
             if l.bn is not None:
-                ops.bn_forward(ops.bn_desc(self.Z[i], self.A[i], l.cout, l.bn_state, l.bn, slope=SLOPE), l.bn_state)
+                d = ops.bn_desc(self.Z[i], self.A[i], l.cout, l.bn_state, l.bn, slope=SLOPE)
+                ops.bn_forward(d, l.bn_state)
+                if REUSE:
+                    if getattr(l, "fwd_acc", None) is None:
+                        l.fwd_acc = torch.empty_like(l.bn_state.acc)
+                    l.fwd_acc.copy_(l.bn_state.acc)  # this batch's sums, for a replayed running update
                 if l.bn.num_batches_tracked is not None:
                     l.bn.num_batches_tracked.add_(1)
+            self._bn_descs.append(d)
             prev = self.A[i]
         return ops.blocked_to_nchw(self.A[-1], torch.empty(self.feat_shape, device=self.device))
 
@@ -292,7 +329,13 @@ def conv_stack_train(dis: nn.Module, x: torch.Tensor) -> torch.Tensor:
     key = (n, h, w, str(x.device))
     pool = dis.__dict__.setdefault("_isr_plans", {})
     plans = pool.setdefault(key, [])
-    plan = next((p for p in plans if not p.busy), None)
+    # prefer an idle plan whose stored forward this call repeats (see DiscriminatorPlan.forward)
+    plan = None
+    if REUSE and len(plans) > 1:
+        plan = next((p for p in plans if not p.busy and getattr(p, "_fwd_key", None) is not None
+                     and p._fwd_key == p._input_key(x)), None)
+    if plan is None:
+        plan = next((p for p in plans if not p.busy), None)
     if plan is None:
         if len(plans) >= 8:
             raise RuntimeError("discriminator: more than 8 live forward graphs")

@@ -143,6 +143,7 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["step"] += 1
+                p.__dict__["_isr_wv"] = p.__dict__.get("_isr_wv", 0) + 1  # raw-pointer write: no _version bump
                 by_step.setdefault(float(st["step"]), []).append(
                     (p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel()))
             for t, rows in by_step.items():

@@ -197,3 +197,37 @@ def test_discriminator_vs_reference_golden(golden):
     for k in g:
         if k.startswith("stat:"):
             assert _rel(bufs[k[5:]], t(g[k]).to(DEV)) < 2e-2, k
+
+
+def test_repeated_forward_reuses_activations_exactly(monkeypatch):
+    """SRGAN's D step repeats the G step's D(sr) (train.py:104 / :126, D not yet updated): the
+    plan reuses its stored activations and replays only the BatchNorm running update.  Outputs,
+    running statistics and the following backward must equal two full recomputations; a weight
+    change (the D optimiser step) or a new input must recompute."""
+    torch.manual_seed(3)
+    base = models.Discriminator(3, 64, 8, 1024).to(DEV).train()
+    x = torch.rand(2, 3, 64, 64, device=DEV) * 2 - 1
+
+    def run(reuse):
+        monkeypatch.setattr(D, "REUSE", reuse)
+        m = copy.deepcopy(base)
+        m.requires_grad_(False)  # the G step: D frozen, input gradient only; the backward frees the plan
+        xg = x.clone().requires_grad_(True)
+        o1 = D.conv_stack_train(m, xg)
+        o1.sum().backward()
+        m.requires_grad_(True)  # the D step: D(sr.detach()) on the same storage
+        o2 = D.conv_stack_train(m, xg.detach())
+        g = torch.autograd.grad(o2.sum(), next(m.parameters()))[0]
+        stats = [(b.running_mean.clone(), b.running_var.clone(), int(b.num_batches_tracked))
+                 for b in m.modules() if isinstance(b, torch.nn.BatchNorm2d)]
+        with torch.no_grad():  # a weight change must force a recompute
+            next(m.parameters()).mul_(0.5)
+        o3 = D.conv_stack_train(m, x)
+        return o1, o2, g, stats, o3
+
+    r, f = run(True), run(False)
+    assert torch.equal(r[0].detach(), f[0].detach()) and torch.equal(r[1].detach(), f[1].detach())
+    assert torch.equal(r[2], f[2])
+    for (m1, v1, n1), (m2, v2, n2) in zip(r[3], f[3]):
+        assert torch.equal(m1, m2) and torch.equal(v1, v2) and n1 == n2
+    assert torch.equal(r[4].detach(), f[4].detach())
