@@ -335,7 +335,7 @@ int isr_wgrad3x3_variant(const isr_wgrad_desc* d, int32_t variant, void* workspa
     int rc = wgrad_validate(d);
     if (rc != ISR_OK) return rc;
     if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null workspace");
-    if (variant < 0 || variant > 13) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: no variant %d", variant);
+    if (variant < 0 || variant > 14) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: no variant %d", variant);
     rc = isr::wgrad3x3_dispatch(d, variant, workspace, ws_bytes, (hipStream_t)s);
     if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: workspace of %zu bytes is smaller than %zu", ws_bytes,
                               isr::wgrad3x3_workspace_bytes(d, variant));
@@ -350,7 +350,7 @@ int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_
 }
 
 size_t isr_wgrad3x3_variant_workspace_bytes(const isr_wgrad_desc* d, int32_t variant) {
-    if (wgrad_validate(d) != ISR_OK || variant < 0 || variant > 13) return 0;
+    if (wgrad_validate(d) != ISR_OK || variant < 0 || variant > 14) return 0;
     return isr::wgrad3x3_workspace_bytes(d, variant);
 }
 

@@ -459,6 +459,14 @@ static auto pick_cw(const isr_wgrad_desc* d, F&& f, bool* ok) {
 template <class F>
 static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
     switch (variant) {
+        case 14: {  // ci-split forms for the discriminator's wide layers (64 co x 128 ci per block)
+            if (d->cout % 64 == 0 && d->ha % 4 == 0) {
+                if (d->taps == 1 && d->cin % 128 == 0) return f(WG<2, 4, 4, 1, 1, 4>());
+                if (d->taps == 0 && d->cin % 128 == 0 && !d->g_sub2) return f(WG<2, 4, 4, 1, 0, 4>());
+                if (d->taps == 0 && d->cin % 64 == 0 && !d->g_sub2) return f(WG<2, 2, 4, 1, 0, 2>());
+            }
+            break;
+        }
         case 12:
         case 13: {
             bool ok;
@@ -481,6 +489,13 @@ static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
     }
     switch (0) {
         default:
+            // the discriminator's wide layers (variant 14: -0.5 % per SRGAN step, same-box A/B): 64 co x
+            // 128 (or 64) ci per block, 8-12 waves splitting the ci tiles, each pixel tile staged once
+            if (d->cout % 64 == 0 && d->ha % 4 == 0 && !d->g_sub2) {
+                if (d->taps == 1 && d->cin % 128 == 0) return f(WG<2, 4, 4, 1, 1, 4>());
+                if (d->taps == 0 && d->cout >= 128 && d->cin % 128 == 0) return f(WG<2, 4, 4, 1, 0, 4>());
+                if (d->taps == 0 && d->cout >= 128 && d->cin % 64 == 0) return f(WG<2, 2, 4, 1, 0, 2>());
+            }
             if (d->taps == 1) return f(WG<1, 1, 8, 2, 1>());  // stride-2 phase conv: taps {0,1}^2, 4 waves
             // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles; 4-row
             // stages when cin % 64 == 32 (96, 160), else 8-row stages with 2 waves per kernel

@@ -6,6 +6,8 @@ CUDA (HIP) tensors and raise otherwise.
 """
 from __future__ import annotations
 
+import os as _os
+
 import ctypes
 from dataclasses import dataclass
 
@@ -361,8 +363,17 @@ def wgrad3x3_desc(x: ActBuffer, cin: int, g: ActBuffer, cout: int, dw: torch.Ten
     return d
 
 
+_WGRAD_VARIANT = int(_os.environ.get("ISR_WGRAD_VARIANT", "0"))  # A/B only (isr_wgrad3x3_variant)
+
+
 def launch_wgrad3x3(d: IsrWgradDesc, device) -> None:
     lib = _lib.load()
+    if _WGRAD_VARIANT:
+        nbytes = lib.isr_wgrad3x3_variant_workspace_bytes(ctypes.byref(d), _WGRAD_VARIANT)
+        ws = _WS.get(max(nbytes, 16), device)
+        check(lib.isr_wgrad3x3_variant(ctypes.byref(d), _WGRAD_VARIANT, ws.data_ptr(), ws.numel(), _stream()),
+              "isr_wgrad3x3_variant")
+        return
     nbytes = lib.isr_wgrad3x3_workspace_bytes(ctypes.byref(d))
     if nbytes == 0:
         check(lib.isr_wgrad3x3(ctypes.byref(d), None, 0, _stream()), "isr_wgrad3x3")

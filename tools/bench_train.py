@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--hr", type=int, default=512)
     ap.add_argument("--blocks", type=int, default=16)
     ap.add_argument("--mode", default="srgan", choices=["srgan", "pixel"])
+    ap.add_argument("--torch-profile", action="store_true", help="print the PyTorch copy/fill ops per step")
     ap.add_argument("--dis-layout", default="nhwc", choices=["nchw", "nhwc"],
                     help="discriminator memory format (stock MIOpen convs)")
     ap.add_argument("--dis-miopen", action="store_true", help="discriminator conv stack on stock MIOpen convs")
@@ -91,6 +92,18 @@ def main():
                           steps=n, log_every=10 ** 9)
     run(args.warmup)
     torch.cuda.synchronize()
+    if args.torch_profile:  # which PyTorch ops (copies / fills) a step issues, with call sites
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+            run(args.steps)
+            torch.cuda.synchronize()
+        keys = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::clone", "aten::add_", "aten::mul", "aten::sub",
+                "aten::add", "aten::div")
+        rows = sorted((e for e in prof.key_averages(group_by_stack_n=5) if e.key in keys), key=lambda e: -e.count)
+        for e in rows[:30]:
+            site = " <- ".join(f.strip().split(" ")[-1][-60:] for f in e.stack[:5])
+            print(f"{e.count / args.steps:7.1f}/step {e.key:14s} {site}")
+        return
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
