@@ -183,6 +183,9 @@ def main():
         elapsed = tt.item()
 
     ms = elapsed / args.steps * 1e3
+    for p in (plan.subs if n_streams > 1 else [plan]):  # a persistent-chain wait that gave up voids the run
+        if p.chain is not None and p.chain.failed():
+            raise engine.ChainFailed("bench: a chain dependency wait gave up during the timed steps")
     hr_px = n * (hw * S) * (hw * S)
     mpix_s = world * hr_px * args.steps / elapsed / 1e6
     # Per-kernel roofline, after the timed region.  The production forward's dominant kernel

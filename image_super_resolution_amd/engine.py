@@ -230,7 +230,14 @@ class GeneratorPlan:
                 ops.check(rc, f"{tag[0]} launch")
             if ev is not None:
                 ev[1].record()
+        if self.chain is not None and not torch.cuda.is_current_stream_capturing():
+            self.chain.poll()
         return out
+
+
+class ChainFailed(RuntimeError):
+    """A persistent-chain dependency wait gave up (a neighbour tile never published: the
+    launch was not fully resident) — that launch's outputs are invalid."""
 
 
 class ConvChain:
@@ -268,6 +275,25 @@ class ConvChain:
         """True when a dependency wait gave up in the last launch (results invalid)."""
         gen, fail = self.state[:2].tolist()
         return gen != 0 and fail == gen
+
+    def poll(self) -> None:
+        """Lagged, non-blocking failure check for the product path: raises ChainFailed when an
+        earlier launch's (generation, give-up) words — copied asynchronously to pinned memory
+        after it — show a wait that gave up; then queues the copy for the launch just issued.
+        Never synchronises (an unfinished copy is checked on a later call)."""
+        ev = getattr(self, "_poll_ev", None)
+        if ev is not None and ev.query():
+            gen, fail = self._poll_host.tolist()
+            if gen != 0 and fail == gen:
+                raise ChainFailed("conv chain: a dependency wait gave up (launch not fully resident); "
+                                  "outputs of that forward are invalid")
+        elif ev is not None:
+            return  # the previous copy has not landed yet: keep it, check it later
+        if getattr(self, "_poll_host", None) is None:
+            self._poll_host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+            self._poll_ev = torch.cuda.Event()
+        self._poll_host.copy_(self.state[:2], non_blocking=True)
+        self._poll_ev.record()
 
 
 class SplitGeneratorPlan:

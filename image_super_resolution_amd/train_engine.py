@@ -449,6 +449,8 @@ class GeneratorTrainPlan:
             rc = e[0](byref(e[1]), st)
             if rc != 0:
                 ops.check(rc, "train forward")
+        if self.chain is not None:
+            self.chain.poll()  # lagged, non-blocking give-up check (engine.ConvChain.poll)
         if self.bn_counters:
             torch._foreach_add_(self.bn_counters, 1)  # nn.BatchNorm2d.train() bookkeeping
         self.y = y

@@ -66,3 +66,28 @@ def test_chain_repeated_stress_eresnet():
     for _ in range(5):
         for out, ref in zip(_run(gw, xs, chain=True), refs):
             assert torch.equal(out, ref)
+
+
+def test_chain_poll_reports_a_give_up():
+    """The product path's lagged check (engine.ConvChain.poll, called by GeneratorPlan.run):
+    a launch whose dependency wait gave up (simulated: give-up word = generation) raises on a
+    later call instead of passing silently."""
+    from image_super_resolution_amd import engine, models
+    from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_state_dict
+    dev = torch.device("cuda")
+    sd = synth_state_dict(models.ResNet(1, 0.2, scaleRate=4).state_dict(), seed=0)
+    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev)
+    lr, _ = synth_lr_batch(2, 32, 32, seed=1)
+    x = normalize(lr).to(dev).contiguous()
+    plan = engine.GeneratorPlan(gw, 2, 32, 32, dev, False, False, (0.485, 0.456, 0.406), (0.229, 0.224, 0.225),
+                                chain=True)
+    out = torch.empty(plan.out_shape, device=dev)
+    plan.run(x, out)
+    torch.cuda.synchronize()
+    plan.run(x, out)  # clean launches: no error
+    torch.cuda.synchronize()
+    plan.chain.state[1] = plan.chain.state[0]  # as if the last launch's wait had given up
+    plan.chain._poll_host.copy_(plan.chain.state[:2])
+    torch.cuda.synchronize()
+    with pytest.raises(engine.ChainFailed):
+        plan.run(x, out)
