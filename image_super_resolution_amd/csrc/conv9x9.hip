@@ -1341,7 +1341,15 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
         }
     }
     if (variant == 5) {
-        int sh = 128;
+        // segment height: the longest walk (<= 512 rows) that still gives every CU a strip —
+        // fewer, longer walks recompute fewer halo T rows and leave no partial last wave of
+        // blocks: 16x512^2 fp32 179 us at 128 rows, 164 at 256, 157 at 512 (tools/tune_tail.py
+        // with ISR_TAIL_SH, profiles/r02_tail_sh.jsonl)
+        int sh = 512;
+        while (sh > 8 && (d->ha % sh || (long)d->n * (d->wa / tail8w::TW) * (d->ha / sh) < cu_count())) sh >>= 1;
+#ifdef ISR_TUNING
+        if (const char* e = getenv("ISR_TAIL_SH")) sh = atoi(e);  // segment-height probe (tuning builds)
+#endif
         while (d->ha % sh) sh >>= 1;
         if (sh < 8) return -2;
         const int blocks = d->n * (d->wa / tail8w::TW) * (d->ha / sh);
