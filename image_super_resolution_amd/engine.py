@@ -187,7 +187,7 @@ class GeneratorPlan:
                 extra = dict(r2=X, s2=ar) if r == 2 else {}
                 c3(src, blk[r][4], dst, slope=1.0, r1=src, s1=ar, **extra)
         self.chain = None
-        if chain and gw.rdb and not variants:
+        if chain and gw.rdb and all(e[3] is None for e in L[trunk0:]):  # variants may only touch other layers
             # the whole RRDB trunk as ONE persistent launch (isr_conv_chain): tile-level
             # dependencies instead of 240 kernel boundaries
             try:
