@@ -135,6 +135,9 @@ SIGNATURES = {
     "isr_conv3x3_check": (c_int32, [POINTER(IsrConvDesc)]),
     "isr_conv_chain_state_words": (c_size_t, [c_int32, c_int32, c_int32]),
     "isr_conv_chain": (c_int32, [POINTER(IsrChainDesc), c_void_p]),
+    "isr_conv_chain_variant": (c_int32, [POINTER(IsrChainDesc), c_int32, c_void_p]),
+    "isr_tuning_trunk_stamps": (c_int32, [c_void_p]),
+    "isr_tuning_trunk_knobs": (c_int32, [c_int32, c_int32, c_int32, c_int32]),
     "isr_head9x9_fwd": (c_int32, [POINTER(IsrHeadDesc), c_void_p]),
     "isr_tail9x9_fwd": (c_int32, [POINTER(IsrTailDesc), c_void_p]),
     "isr_tail9x9_fwd_variant": (c_int32, [POINTER(IsrTailDesc), c_int32, c_void_p]),

@@ -15,6 +15,10 @@ int chain_knobs_set(const int* k);
 int tail_stamps_set(void* p);
 size_t conv_chain_state_words(int n, int ha, int wa);
 int conv_chain(const isr_chain_desc* c, hipStream_t s);
+size_t trunk_state_words(int n, int ha, int wa);
+int trunk_launch(const isr_chain_desc* c, hipStream_t s);
+int trunk_stamps_set(void* p);
+int trunk_knobs_set(const int* k);
 size_t conv3x3_packed_bytes(int cout, int cin);
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s);
@@ -222,15 +226,38 @@ int isr_conv3x3_check(const isr_conv_desc* d) { return conv3x3_validate(d); }
 
 size_t isr_conv_chain_state_words(int32_t n, int32_t ha, int32_t wa) {
     if (n <= 0 || ha <= 0 || wa <= 0 || ha % 16 || wa % 32) return 0;
-    return isr::conv_chain_state_words(n, ha, wa);
+    const size_t a = isr::conv_chain_state_words(n, ha, wa), b = isr::trunk_state_words(n, ha, wa);
+    return a > b ? a : b;
 }
 
-int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s) {
-    if (!c || !c->layers || !c->kinds || !c->state || c->nl <= 0)
-        return fail(ISR_ERR_BAD_DESC, "conv chain: null layers / kinds / state or nl <= 0");
+int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s) {
+    if (!c || !c->layers || !c->kinds || !c->state || c->nl <= 0 || c->nl > 1024)
+        return fail(ISR_ERR_BAD_DESC, "conv chain: null layers / kinds / state or nl not in [1, 1024]");
     if (c->n <= 0 || c->ha <= 0 || c->wa <= 0 || c->ha % 16 || c->wa % 32)
         return fail(ISR_ERR_BAD_DESC, "conv chain: bad grid n=%d ha=%d wa=%d", c->n, c->ha, c->wa);
-    return launched(isr::conv_chain(c, (hipStream_t)s), "conv chain");
+    if (variant == 0) {
+        const int rc = isr::trunk_launch(c, (hipStream_t)s);
+        if (rc == -4) return fail(ISR_ERR_LAUNCH, "conv chain: the occupancy query admits no workgroup per CU");
+        if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "conv chain: unsupported grid or layer count");
+        return launched(rc, "conv chain");
+    }
+    if (variant == 1) return launched(isr::conv_chain(c, (hipStream_t)s), "conv chain (round-2 kernel)");
+    return fail(ISR_ERR_UNSUPPORTED, "conv chain: unknown variant %d", variant);
+}
+
+int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s) { return isr_conv_chain_variant(c, 0, s); }
+
+int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k3) {
+    const int k[4] = {ablate, per_cu, k2, k3};
+    const int rc = isr::trunk_knobs_set(k);
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "trunk knobs: library built without -DISR_TUNING");
+    return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "trunk knobs: hipMemcpyToSymbol failed");
+}
+
+int isr_tuning_trunk_stamps(void* buf) {
+    const int rc = isr::trunk_stamps_set(buf);
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "trunk stamps: library built without -DISR_TUNING");
+    return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "trunk stamps: hipMemcpyToSymbol failed");
 }
 
 int isr_tuning_conv_stamps(void* buf) {

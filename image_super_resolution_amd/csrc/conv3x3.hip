@@ -20,6 +20,8 @@
 // The epilogue transposes one output row at a time through LDS so that every
 // lane stores 16 contiguous bytes (8 channels) of one pixel.
 // Grid: 1D, XCD-aware (xcd_remap) with the cout tile innermost, then x, y, image.
+#include <string.h>
+
 #include "isr_common.h"
 
 namespace isr {
@@ -52,9 +54,12 @@ __device__ __forceinline__ void conv_stamp(int slot, int row = -1) {
 }
 
 template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1), int EPQ_ = 4,
-          int SPL_ = 0, int TWN_ = 0, int NSW_ = 0>
+          int SPL_ = 0, int TWN_ = 0, int NSW_ = 0, int FOLD_ = 0>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
+    // 1: the RDB residual fold (r1 == the conv's own input channels, see fold_ok) is compiled in;
+    // only the RDB final-conv instantiations carry it (it costs registers)
+    static constexpr int FOLD = FOLD_;
     // 1: double-buffered fragment registers across (k-step, dx) steps; 2: the next step's reads
     // spread over the current step's MFMAs (front-loading them instead: 0.43-0.92x, register
     // pressure)
@@ -107,11 +112,32 @@ struct C3 {
     static_assert(KC == 16 || KC == 32, "chunk width");
 };
 
-__device__ __forceinline__ void swap_halves(float& lo, float& hi) {
-    // v_permlane32_swap: lanes 32..63 of `lo` trade places with lanes 0..31 of `hi`
-    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
-    lo = __uint_as_float(r[0]);
-    hi = __uint_as_float(r[1]);
+// A operand of the residual fold: (1/s1) I on couts [16 h16, 16 h16 + 16) of a 32-cout
+// fragment (lane l supplies A[l & 31][8 (l >> 5) .. + 8]); trunk.hip builds the same.
+__device__ __forceinline__ bf16x8 fold_a(float s1, int h16) {
+    const __bf16 bi = (__bf16)(1.f / s1);
+    const unsigned idv = __builtin_bit_cast(uint16_t, bi);
+    const int lane = threadIdx.x & 63;
+    const int j = (lane & 31) - 16 * h16 - 8 * (lane >> 5);
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    u32x4 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = j == 2 * k ? idv : (j == 2 * k + 1 ? idv << 16 : 0u);
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+// The fold applies when r1 is exactly the conv's own input channels [0, cout) (one cout tile),
+// the activation is the identity and 1/s1 is exact in bf16 (add_rate 0.2 → 5).
+template <class C, bool XS2, class Desc>
+__device__ __forceinline__ bool fold_ok(const Desc& d) {
+    if constexpr (!C::FOLD || C::NF != 2 || C::KS != 1 || C::TN != 3 || C::PIPE != 2 || XS2) {
+        return false;
+    } else {
+        if (!d.r1.data || d.r1.data != d.x.data || d.r1.coff != d.x.coff || d.r1_cn != 0) return false;
+        if (d.cout != C::CT || d.slope != 1.f || d.y2.data || d.m.data || d.shuffle != 1) return false;
+        const float inv = 1.f / d.s1;
+        return (float)(__bf16)inv == inv;
+    }
 }
 
 // Epilogue.  Accumulators are D[cout][pixel]: lane l owns pixel l31 of the row
@@ -239,6 +265,7 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
+                    if constexpr (MODE & 32) u[e] = u[e] * d.s1;
                     if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (use_r1 ? (float)q1[cb][blk][e] : 0.f);
                     if constexpr (MODE & 2) {
                         u[e] = u[e] * d.s2 + (float)q2[cb][blk][e];
@@ -293,6 +320,11 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
     const int l31 = lane & 31;
     const int hh = lane >> 5;
     const int nchunks = C::CIN ? C::CIN / C::KC : d.cin / C::KC;
+    // RDB residual fold (trunk.hip): when r1 is the conv's own input channels [0, cout) and the
+    // activation is the identity, x/s1 is added by extra MFMAs on the staged centre pixels
+    // (A = (1/s1) I, exact in bf16) and the epilogue computes acc * s1 — no r1 re-read.  The
+    // same MFMA order as trunk.hip's kernel, so every path stays bit-identical.
+    const bool fold = fold_ok<C, XS2>(d);
     conv_stamp(0, srow);
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
@@ -514,7 +546,7 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
                 int m = 0;
 
 #pragma unroll
-                for (int ia = 0; ia < NA; ++ia)
+                for (int ia = 0; ia < NA; ++ia) {
 #pragma unroll
                     for (int dyi = 0; dyi < TN; ++dyi) {
                         const int r = ia - dyi;
@@ -529,6 +561,17 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
                             }
                         }
                     }
+                    if constexpr (C::FOLD && C::NF == 2 && C::KS == 1 && C::TN == 3) {
+                        // residual fold: + x/s1 on the centre pixels of output row ia - 1 (dx = 1,
+                        // dy = 1), right after input row ia's MFMAs (trunk.hip's order)
+                        if (st == 1 && fold && chunk < 4 && ia >= 1 && ia <= R) {
+                            const bf16x8 a = fold_a(d.s1, chunk & 1);
+                            if (chunk < 2) acc[ia - 1][0] = mfma32(a, fa[cur][ia], acc[ia - 1][0]);
+                            else acc[ia - 1][1] = mfma32(a, fa[cur][ia], acc[ia - 1][1]);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    }
+                }
                 continue;
             } else if constexpr (C::PIPE) {
                 if (st + 1 < NS) load_step(st + 1, cur ^ 1);
@@ -577,12 +620,17 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
     }
     // ---- epilogue (mode picked once, wave-uniform, so no per-element branches)
     const int mode = d.shuffle == 2 ? (d.m.data ? 24 : 8)
-                                    : ((d.r1.data ? 1 : 0) | (d.r2.data ? 2 : 0) | (d.y2.data ? 4 : 0) | (d.m.data ? 16 : 0));
-    if constexpr (HX) {  // chain layers: growth (plain store) or the RDB final conv (r1 [+ r2])
+                     : fold ? (32 | (d.r2.data ? 2 : 0))
+                            : ((d.r1.data ? 1 : 0) | (d.r2.data ? 2 : 0) | (d.y2.data ? 4 : 0) | (d.m.data ? 16 : 0));
+    if constexpr (HX) {  // chain layers: growth (plain store) or the RDB final conv (folded r1 [+ r2])
         if (mode == 0) epilogue<C, 0, HX>(d, acc, img, ct, x0, y0, wave, lane);
+        else if (mode == 32) epilogue<C, 32, HX>(d, acc, img, ct, x0, y0, wave, lane);
+        else if (mode == 34) epilogue<C, 34, HX>(d, acc, img, ct, x0, y0, wave, lane);
         else if (mode == 1) epilogue<C, 1, HX>(d, acc, img, ct, x0, y0, wave, lane);
         else epilogue<C, 3, HX>(d, acc, img, ct, x0, y0, wave, lane);
     } else switch (mode) {
+        case 32: epilogue<C, 32, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
+        case 34: epilogue<C, 34, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 0: epilogue<C, 0, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 1: epilogue<C, 1, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
         case 2: epilogue<C, 2, HX>(d, acc, img, ct, x0, y0, wave, lane); break;
@@ -651,6 +699,19 @@ using V_W1 = C3<4, 8, 2, 16, 2>; // 32x32 px tile, 8 waves, KC16 double buffer
 using V_W2 = C3<2, 4, 2, 32, 2>; // 8x32, KC32
 using V_W3 = C3<2, 4, 2, 16, 2, 0, 0, 2>; // 8x32 tile, interleaved
 using V_F0 = C3<4, 4, 2, 16, 2, 192, 0, 2>; // RDB final conv 192→64: V_W0 with compile-time cin, PIPE 2
+using V_F0F = C3<4, 4, 2, 16, 2, 192, 0, 2, 4, 0, 0, 0, 1>; // V_F0 with the residual fold (r1 == x)
+
+// Host mirror of fold_ok: r1 is the conv's own input channels [0, cout), identity activation,
+// 1/s1 exact in bf16 (its low 16 fp32 bits zero).
+static bool fold_host(const isr_conv_desc* d) {
+    if (!d->r1.data || d->r1.data != d->x.data || d->r1.coff != d->x.coff || d->r1_cn != 0) return false;
+    if (d->cout != 64 || d->slope != 1.f || d->y2.data || d->m.data || d->shuffle != 1 || d->x_sub2 || d->taps)
+        return false;
+    const float inv = 1.f / d->s1;
+    uint32_t bits;
+    memcpy(&bits, &inv, 4);
+    return (bits & 0xffffu) == 0;
+}
 
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
     if (d->cout % 64) {  // 32-cout tiles: growth convs (cout 32) and dgrad of them (96, 160)
@@ -672,7 +733,8 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
         return -2;
     }
     switch (variant) {
-        case 0: return d->cin == 192 ? launch3x3<V_F0, true>(d, s) : launch3x3<V_W0, true>(d, s);
+        case 0: return d->cin == 192 ? (fold_host(d) ? launch3x3<V_F0F>(d, s) : launch3x3<V_F0, true>(d, s))
+                                     : launch3x3<V_W0, true>(d, s);
         case 1: return launch3x3<V_W1>(d, s);
         case 2: return launch3x3<V_W2>(d, s);
         case 3: return launch3x3<V_W3>(d, s);
@@ -927,7 +989,7 @@ int conv_chain(const isr_chain_desc* c, hipStream_t s) {
     // production: the dependency wait runs after the tile's scalar setup (its descriptor loads —
     // three dependent scalar round trips, ~2.4 µs per tile — overlap the wait): -1.2 % per
     // forward against waiting first (tools/chain_probe.py, variant 0 vs 5)
-    return launch_chain<V_G0, V_F0, 1>(c, s);
+    return launch_chain<V_G0, V_F0F, 1>(c, s);
 }
 
 #ifdef ISR_TUNING

@@ -25,6 +25,13 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 acc) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
 }
 
+__device__ __forceinline__ void swap_halves(float& lo, float& hi) {
+    // v_permlane32_swap: lanes 32..63 of `lo` trade places with lanes 0..31 of `hi`
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+    lo = __uint_as_float(r[0]);
+    hi = __uint_as_float(r[1]);
+}
+
 __device__ __forceinline__ bf16x8 lds_read16(const char* p) {
     return *reinterpret_cast<const bf16x8*>(p);
 }

@@ -1,0 +1,760 @@
+// The RRDB trunk (utils/models.py:298-317 RRDB.forward over :245-271 RDB.forward, the
+// `nn.Sequential(*RRDB)` of ResNet/EResNet :598 / :627) as ONE persistent launch: every RDB
+// conv (4 growth convs 64+32k -> 32 + LeakyReLU; the final 192 -> 64 conv with the RDB and
+// RRDB residuals) of every block, with tile-level dependencies instead of kernel boundaries.
+//
+// Round-3 design.  The round-2 chain (conv3x3.hip conv_chain_kernel) ran every (layer, tile)
+// as an independent conv tile: descriptor round trips, a pipeline fill, the dependency wait,
+// the pipeline drain, the store drain — per tile and per layer, ~45 % of every RDB.  Here a
+// workgroup runs ONE continuous stream of K-chunks over its (layer, tile) items:
+//  * the 2-slot LDS ring never drains at a tile or layer boundary: the first chunk of the next
+//    (layer, tile) is staged by LDS-DMA while the current tile's last chunk computes;
+//  * a tile starts on the K-chunks its previous layer did NOT write (an RDB conv reads the
+//    block input and the older growth outputs, which the previous layer's stencil wait already
+//    covered) and waits for its 3x3 tile neighbourhood only before staging the first chunk the
+//    previous layer wrote (`first_new`); that poll is issued one chunk ahead of the refill;
+//  * no per-tile descriptor chain: a 64-byte layer record (compiled on the device from the
+//    caller's isr_conv_desc table by trunk_prep_kernel) is read through the scalar cache, the
+//    bias is staged into LDS with the first chunk;
+//  * the RDB residual r1 = x[0:64] (the conv's own input) is added by four extra MFMAs per chunk
+//    on the already-staged centre pixels (A = (1/s1) I, exact in bf16 for add_rate 0.2) instead
+//    of re-reading 64 KB per tile in the epilogue: out = (acc + x/s1) * s1.  conv3x3.hip applies
+//    the same fold at the same point of the same MFMA order, so the per-conv launches and the
+//    round-2 chain stay bit-identical to this kernel.
+// Hand-off (cdna_hip_programming.md Guideline 16, R1): write-through (sc1) output stores,
+// drained by every wave before a workgroup barrier and a relaxed agent-scope progress store;
+// consumers poll the 9 neighbour words (sc1 loads, per wave) and read activations with sc1
+// LDS-DMA.  Progress words are serial numbers gen * 1024 + layers done (no zeroing per call).
+#include "isr_common.h"
+
+namespace isr {
+
+namespace tk {
+constexpr int R = 4;            // output rows per wave
+constexpr int WM = 4;           // waves per workgroup
+constexpr int NT = 64 * WM;
+constexpr int TH = R * WM;      // 16-row tile
+constexpr int TW = 32;
+constexpr int HR = TH + 2, HC = TW + 2, HQ = HR * HC;  // 18 x 34 halo pixels
+constexpr int HP = (HQ + 31) / 32;                      // 20 halo pieces (1 KB) per chunk
+constexpr int HPW = HP / WM;                            // 5 per wave
+static_assert(HP % WM == 0, "halo pieces per wave");
+constexpr int WPG = 9, WPF = 18;                        // weight pieces per chunk: 32 / 64 couts
+constexpr int SLOT = (HP + WPF) * 1024;                 // 38 KB ring slot
+constexpr int BIAS_OFF = 2 * SLOT;                      // 2 x 256 B bias slots
+constexpr int FLAG_OFF = BIAS_OFF + 512;                // per-wave "refill deferred" words
+constexpr int LDS = FLAG_OFF + 16;
+constexpr int NEED_NONE = 255;
+}  // namespace tk
+
+// Layer record (64 bytes at state words [rec_off + 16 L, + 16)), dwords only: a scalar load
+// cannot fetch bytes on gfx950, so packed small fields are unpacked with scalar shifts.
+struct TrunkRec {
+    uint64_t x, y, w, b, r2;   // buffer bases, packed weights, fp32 bias, r2 base (or 0)
+    uint32_t planes;           // xp | yp << 16: first 16-channel plane of x / y (coff / 16)
+    uint32_t shape;            // r2p | nch << 16 | kind << 24 (nch = cin / 16; kind 0 growth, 1 final)
+    uint32_t deps;             // first_new | fold << 8 | idv << 16 (first chunk the previous layer
+                               // wrote, NEED_NONE on layer 0; fold: r1 == x[0:cout] added as x/s1
+                               // by MFMA; idv: bf16 bits of 1/s1)
+    float slope, s1, s2;
+};
+static_assert(sizeof(TrunkRec) == 64, "record size");
+
+// Geometry (16 words just before the layer records), shared by every layer.
+struct TrunkGeo {
+    int32_t n, h, w, ha, wa, hp, wp, cs16, pad, nbx, nby, ntiles, err, r0, r1, r2;
+};
+
+static inline __host__ __device__ size_t trunk_rec_off(int ntiles) {
+    return ((size_t)ntiles + 4 + 15) / 16 * 16 + 16;  // words; geometry at rec_off - 16
+}
+
+size_t trunk_state_words(int n, int ha, int wa) {
+    const size_t tiles = (size_t)n * (ha / tk::TH) * (wa / tk::TW);
+    return trunk_rec_off((int)tiles) + 1024 * 16;
+}
+
+// ---- prep: validate the layer table and compile it into records; bump the generation ----
+// err bits: 1 grid, 2 view geometry, 4 kind/cout, 8 cin/bias, 16 unsupported epilogue form,
+// 32 residual form, 64 beyond the 2 GiB buffer window, 128 too many layers.
+__global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* layers, const int32_t* kinds, int nl,
+                                                          int n, int ha, int wa, unsigned* state) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    unsigned* err = reinterpret_cast<unsigned*>(smem);
+    const int L = threadIdx.x;
+    const int nbx = wa / tk::TW, nby = ha / tk::TH, ntiles = n * nbx * nby;
+    const size_t ro = trunk_rec_off(ntiles);
+    if (L == 0) *err = 0;
+    __syncthreads();
+    const isr_conv_desc& g0 = layers[0];
+    if (L < nl) {
+        const isr_conv_desc& d = layers[L];
+        unsigned e = 0;
+        auto same_geo = [&](const isr_view& v) {
+            return v.hp == g0.x.hp && v.wp == g0.x.wp && v.cs == g0.x.cs && v.pad == g0.x.pad && v.coff % 16 == 0 &&
+                   v.pad >= 1;
+        };
+        const int kind = kinds[L];
+        if (d.n != n || d.ha != ha || d.wa != wa || d.h != g0.h || d.w != g0.w) e |= 1;
+        if (!same_geo(d.x) || !same_geo(d.y) || (d.r2.data && !same_geo(d.r2))) e |= 2;
+        if (kind == 0 ? d.cout != 32 : (kind == 1 ? d.cout != 64 : true)) e |= 4;
+        if (d.cin % 16 || d.cin < 64 || d.cin / 16 > 120 || !d.bias || ((uintptr_t)d.bias & 15)) e |= 8;
+        if (d.shuffle != 1 || d.x_sub2 || d.taps || d.m.data || d.y2.data) e |= 16;
+        int fold = 0;
+        uint16_t idv = 0;
+        if (d.r1.data) {
+            const float inv = 1.f / d.s1;
+            const __bf16 bi = (__bf16)inv;
+            idv = __builtin_bit_cast(uint16_t, bi);
+            const bool alias = d.r1.data == d.x.data && d.r1.coff == d.x.coff && d.r1_cn == 0;
+            if (!alias || kind != 1 || d.slope != 1.f || (float)bi != inv) e |= 32;
+            fold = 1;
+        } else if (d.r2.data) {
+            e |= 32;
+        }
+        int first_new = tk::NEED_NONE;
+        if (L > 0) {
+            const isr_conv_desc& p = layers[L - 1];
+            const int lo = p.y.coff, hi = p.y.coff + p.cout;
+            first_new = d.cin / 16;  // reads nothing the previous layer wrote: wait before storing
+            if (p.y.data == d.x.data) {
+                for (int c = 0; c < d.cin / 16; ++c) {
+                    const int c0 = d.x.coff + 16 * c;
+                    if (c0 < hi && lo < c0 + 16) {
+                        first_new = c;
+                        break;
+                    }
+                }
+            }
+        }
+        TrunkRec rec;
+        rec.x = (uint64_t)(uintptr_t)d.x.data;
+        rec.y = (uint64_t)(uintptr_t)d.y.data;
+        rec.w = (uint64_t)(uintptr_t)d.wpack;
+        rec.b = (uint64_t)(uintptr_t)d.bias;
+        rec.r2 = (uint64_t)(uintptr_t)d.r2.data;
+        rec.planes = (uint32_t)(d.x.coff / 16) | (uint32_t)(d.y.coff / 16) << 16;
+        rec.shape = (uint32_t)(d.r2.coff / 16) | (uint32_t)(d.cin / 16) << 16 | (uint32_t)(kind & 255) << 24;
+        rec.deps = (uint32_t)first_new | (uint32_t)fold << 8 | (uint32_t)idv << 16;
+        rec.slope = d.slope;
+        rec.s1 = d.s1;
+        rec.s2 = d.s2;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&rec);
+        uint32_t* dst = state + ro + (size_t)L * 16;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dst[i] = src[i];
+        if (e) atomicOr(err, e);
+    }
+    __syncthreads();
+    if (L == 0) {
+        const size_t bytes = (size_t)n * (g0.x.cs / 16) * g0.x.hp * g0.x.wp * 32;
+        const unsigned e = *err | (bytes >= 0x7fffffffull ? 64u : 0u) | (nl > 1024 ? 128u : 0u);
+        uint32_t* geo = state + ro - 16;
+        const int32_t gv[16] = {n, g0.h, g0.w, ha, wa, g0.x.hp, g0.x.wp, g0.x.cs / 16, g0.x.pad, nbx, nby, ntiles,
+                                (int32_t)e, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) geo[i] = (uint32_t)gv[i];
+        state[0] = state[0] + 1u;  // this launch's generation (a vector store by one lane)
+    }
+}
+
+// ---- main kernel -------------------------------------------------------------------------
+typedef const __attribute__((address_space(4))) TrunkRec const_rec;
+typedef const __attribute__((address_space(4))) TrunkRec const_rec_t;
+typedef const __attribute__((address_space(4))) TrunkGeo const_geo;
+#ifdef ISR_TUNING
+// per (layer 75..89, tile) 8 stamps: [0] tile entry, [1] chunk 0 landed, [2] main loop done,
+// [3] stores issued, [4] first dependency poll issued, [5] dependency met (s_memrealtime, 100 MHz)
+__device__ unsigned long long* g_trunk_stamps;
+#endif
+__device__ __forceinline__ void trunk_stamp(int L, int t, int ntiles, int slot) {
+#ifdef ISR_TUNING
+    unsigned long long* p = g_trunk_stamps;
+    if (p != nullptr && threadIdx.x == 0 && L >= 75 && L < 90) {
+        unsigned long long v;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+        p[((size_t)(L - 75) * ntiles + t) * 8 + slot] = v;
+    }
+#else
+    (void)L, (void)t, (void)ntiles, (void)slot;
+#endif
+}
+
+__device__ __forceinline__ int rec_xp(const_rec_t& r) { return (int)(r.planes & 0xffff); }
+__device__ __forceinline__ int rec_yp(const_rec_t& r) { return (int)(r.planes >> 16); }
+__device__ __forceinline__ int rec_r2p(const_rec_t& r) { return (int)(r.shape & 0xffff); }
+__device__ __forceinline__ int rec_nch(const_rec_t& r) { return (int)((r.shape >> 16) & 255); }
+__device__ __forceinline__ int rec_kind(const_rec_t& r) { return (int)(r.shape >> 24); }
+__device__ __forceinline__ int rec_first_new(const_rec_t& r) { return (int)(r.deps & 255); }
+__device__ __forceinline__ bool rec_fold(const_rec_t& r) { return ((r.deps >> 8) & 1) != 0; }
+__device__ __forceinline__ uint32_t rec_idv(const_rec_t& r) { return r.deps >> 16; }
+
+// Tuning builds: ablation knobs (timing only, outputs wrong): bit 1 = no halo LDS-DMA after the
+// first item, 2 = no MFMAs (operands kept live), 4 = no epilogue stores; [1] = workgroups per CU
+// (host side, 0 = occupancy).
+#ifdef ISR_TUNING
+__device__ int g_trunk_knobs[4];
+static int g_trunk_per_cu = 0;
+__device__ __forceinline__ int trunk_abl() { return g_trunk_knobs[0]; }
+#else
+__device__ __forceinline__ int trunk_abl() { return 0; }
+#endif
+
+struct TrunkArgs {
+    unsigned* state;
+    int rec_off;   // words
+    int nl;
+    int acquire;
+};
+
+
+__device__ __forceinline__ void raw_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+// 4-byte-per-lane LDS-DMA (the bias: 64 floats = 256 B per wave instruction)
+__device__ __forceinline__ void glds4(const void* gsrc, void* lds) {
+    __builtin_amdgcn_global_load_lds(gsrc, ISR_LDS_PTR(lds), 4, 0, 0);
+}
+
+// Neighbour of tile t polled by this lane (lanes 0..8: the 3x3 neighbourhood), or -1.
+__device__ __forceinline__ int nb_of(int t, int nbx, int nby) {
+    const int lane = threadIdx.x & 63;
+    if (lane >= 9) return -1;
+    const int bx = t % nbx, tmp = t / nbx, by = tmp % nby, img = tmp / nby;
+    const int yy = by + lane / 3 - 1, xx = bx + lane % 3 - 1;
+    return (yy >= 0 && yy < nby && xx >= 0 && xx < nbx) ? (img * nby + yy) * nbx + xx : -1;
+}
+
+__device__ __forceinline__ unsigned poll_load(const unsigned* progress, int nb) {
+    return __hip_atomic_load(progress + (nb < 0 ? 0 : nb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Blocking wave-level wait for the neighbourhood: every lane leaves with the dependency met or
+// the launch given up (bounded spin, then state[1] = gen, and every later wait returns at once
+// so the grid always drains; the host reads state[1] == state[0] as "outputs invalid").
+__device__ __forceinline__ void dep_wait(unsigned* state, int nb, unsigned need, unsigned gen) {
+    const unsigned* progress = state + 4;
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned v = poll_load(progress, nb);
+        if (__all(nb < 0 || (int)(v - need) >= 0)) break;
+        if ((spins & 255) == 255 && __hip_atomic_load(state + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen)
+            break;
+        if (spins > (1u << 18)) {
+            if ((threadIdx.x & 63) == 0) __hip_atomic_store(state + 1, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+__device__ __forceinline__ void acquire_fence() {
+    if ((threadIdx.x & 63) == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Where the chunks of one (layer, tile) item come from (LDS-DMA through buffer resources:
+// 32-bit offsets, no per-piece 64-bit address arithmetic).
+struct Src {
+    const char* x;   // activation buffer base
+    uint32_t h0;     // byte offset of the halo origin of chunk 0: pixel (y0-1, x0-1) of plane xp
+    const char* w;   // packed weights of chunk 0
+    const float* b;  // bias
+    int wpc;         // weight pieces per chunk (9 / 18)
+};
+
+struct TrunkCtx {
+    unsigned* state;
+    unsigned gen;
+    int acquire;
+    int hp, wp, cs16, pad, h, w, nbx, nby, ntiles;
+    uint32_t pstride;            // bytes per 16-channel plane
+    uint32_t hoff[tk::HPW];      // per-lane halo piece offsets (chunk-invariant)
+};
+
+__device__ __forceinline__ Src src_of(const TrunkCtx& c, const_rec& rec, int t) {
+    const int bx = t % c.nbx, tmp = t / c.nbx, by = tmp % c.nby, img = tmp / c.nby;
+    Src s;
+    s.x = (const char*)(uintptr_t)rec.x;
+    s.h0 = (uint32_t)(((((uint32_t)img * c.cs16 + rec_xp(rec)) * c.hp + (by * tk::TH - 1 + c.pad)) * c.wp +
+                       (bx * tk::TW - 1 + c.pad)) * 32);
+    s.w = (const char*)(uintptr_t)rec.w;
+    s.b = (const float*)(uintptr_t)rec.b;
+    s.wpc = rec_kind(rec) == 0 ? tk::WPG : tk::WPF;
+    return s;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// LDS halo image of one chunk: pixel q = row * 34 + col holds 2 units of 16 B (8 channels);
+// unit (q, c) sits at 2q + (c ^ bit 3 of col).  The swizzle depends on the column only, so the
+// rows a wave reads at one dx share one per-lane address (row offsets are immediates), and the
+// 16 lanes of a ds_read_b128 group (columns 8 apart pair up) still hit 16 distinct bank slots.
+__device__ __forceinline__ uint32_t halo_piece_off(int j, int lane, int wp) {
+    const int u = j * 64 + lane;
+    const int q = u >> 1;
+    if (q >= tk::HQ) return 0;  // tail of the last piece: never read
+    const int row = q / tk::HC, col = q - row * tk::HC;
+    const int cc = (u & 1) ^ ((col >> 3) & 1);
+    return (uint32_t)((row * wp + col) * 32 + cc * 16);
+}
+
+// One chunk's LDS-DMA into ring slot `slot`: each wave its share of the 20 halo and 9 / 18
+// weight pieces; wave 0 also the bias (first chunk of a tile).  Halo pieces are sc1 (L1
+// bypass: other workgroups of this launch wrote them).
+__device__ __forceinline__ void stage_chunk(const TrunkCtx& c, const Src& s, int chunk, int slot, bool with_bias,
+                                            int bslot) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    char* dst = smem + slot * tk::SLOT;
+    const auto rx = rsrc(s.x);
+    const uint32_t so = s.h0 + (uint32_t)chunk * c.pstride;
+    if (!(trunk_abl() & 1))
+#pragma unroll
+    for (int k = 0; k < tk::HPW; ++k)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, ISR_LDS_PTR(dst + (wave + tk::WM * k) * 1024), 16, c.hoff[k], so,
+                                                 0, 16);
+    const auto rw = rsrc(s.w);
+    const uint32_t wo = (uint32_t)(chunk * s.wpc * 1024);
+    char* wd = dst + tk::HP * 1024;
+#pragma unroll
+    for (int k = 0; k < (tk::WPF + tk::WM - 1) / tk::WM; ++k) {
+        const int j = wave + tk::WM * k;
+        if (j < s.wpc)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, ISR_LDS_PTR(wd + j * 1024), 16, lane * 16, wo + j * 1024, 0, 0);
+    }
+    if (with_bias && wave == 0 && lane < (s.wpc == tk::WPG ? 32 : 64))  // cout floats only
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(s.b), ISR_LDS_PTR(smem + tk::BIAS_OFF + bslot * 256), 4, lane * 4,
+                                                 0, 0, 0);
+}
+
+// A operand of the residual fold: (1/s1) I on couts [16 h16, 16 h16 + 16) of a 32-cout
+// fragment (lane l supplies A[l & 31][8 (l >> 5) .. + 8]); conv3x3.hip builds the same.
+__device__ __forceinline__ bf16x8 fold_a_bits(uint32_t idv, int h16) {
+    const int lane = threadIdx.x & 63;
+    const int j = (lane & 31) - 16 * h16 - 8 * (lane >> 5);
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    u32x4 r;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) r[d] = j == 2 * d ? idv : (j == 2 * d + 1 ? idv << 16 : 0u);
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+// The item that follows the current tile in this workgroup's stream.
+struct Next {
+    bool exists;
+    int L, t;
+    Src src;
+    int first_new;   // its first chunk its previous layer wrote (0: chunk 0 needs the wait)
+    bool self_dep;   // its neighbourhood contains the tile being computed now
+};
+
+// Carried from item to item.
+struct Stream {
+    int item;        // chunk counter (ring slot = item & 1)
+    int tseq;        // tile counter (bias slot = tseq & 1)
+    bool staged;     // this wave issued the DMA of the next chunk
+    bool mixed;      // that decision came from a per-wave poll (waves may disagree)
+    int pend_t;      // tile whose progress word is still to be published (-1: none)
+    unsigned pend_v;
+    unsigned pollv;  // early poll of the next dependency (issued one chunk ahead)
+    bool polled;
+    bool dep_next;   // this wave verified the next tile's neighbourhood when staging its chunk 0
+};
+
+template <int NF>
+__device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_rec& rec, int L, int t,
+                                         const Next& nx) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int R = tk::R, CT = 32 * NF, TN = 3, NA = R + 2;
+    const int wave = wave_id(), lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+    const int bx = t % c.nbx, tmp = t / c.nbx, by = tmp % c.nby, img = tmp / c.nby;
+    const int x0 = bx * tk::TW, y0 = by * tk::TH;
+    const int nch = rec_nch(rec);
+    const int first_new = rec_first_new(rec);  // NEED_NONE on layer 0
+    const unsigned need = c.gen * 1024u + (unsigned)L;  // the neighbourhood is done with layer L-1
+    const bool fold = NF == 2 && rec_fold(rec);
+    const Src me = src_of(c, rec, t);
+    bool dep_ok = first_new == tk::NEED_NONE || (first_new == 0 && st.dep_next);
+    st.dep_next = false;
+    const int bslot = st.tseq & 1;
+    trunk_stamp(L, t, c.ntiles, 0);
+
+    // per-lane LDS read addresses (slot 0): weights A[n][k] (n = cout), halo rows of this wave
+    const uint32_t a_w = (uint32_t)(tk::HP * 1024 + (2 * l31 + (hh ^ ((l31 >> 3) & 1))) * 16);
+    uint32_t a_h[3];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+        a_h[dx] = (uint32_t)((wave * R * tk::HC + l31 + dx) * 32 + 16 * (hh ^ (((l31 + dx) >> 3) & 1)));
+
+    f32x16 acc[R][NF];
+
+    for (int ch = 0; ch < nch; ++ch, ++st.item) {
+        const int slot = st.item & 1;
+        // ---- top of item: the chunk has landed for every wave; publish the previous tile ----
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (st.mixed) *reinterpret_cast<volatile int*>(smem + tk::FLAG_OFF + 4 * wave) = st.staged ? 0 : 1;
+        raw_barrier();
+        if (st.pend_t >= 0) {
+            if (threadIdx.x == 0)
+                __hip_atomic_store(c.state + 4 + st.pend_t, st.pend_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st.pend_t = -1;
+        }
+        bool any_deferred = !st.staged;
+        if (st.mixed) {
+            const volatile int* fl = reinterpret_cast<const volatile int*>(smem + tk::FLAG_OFF);
+            any_deferred = (fl[0] | fl[1] | fl[2] | fl[3]) != 0;
+        }
+        if (any_deferred) {  // uniform: a deferred refill — wait for the neighbourhood, stage, land
+            if (!st.staged) {
+                if (ch >= first_new && !dep_ok) {
+                    trunk_stamp(L, t, c.ntiles, 4);
+                    dep_wait(c.state, nb_of(t, c.nbx, c.nby), need, c.gen);
+                    if (c.acquire) acquire_fence();
+                    trunk_stamp(L, t, c.ntiles, 5);
+                }
+                stage_chunk(c, me, ch, slot, ch == 0, bslot);
+            }
+            if (ch >= first_new) dep_ok = true;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            raw_barrier();
+        }
+        st.staged = true;
+        st.mixed = false;
+        if (ch == 0) {
+            trunk_stamp(L, t, c.ntiles, 1);
+            // bias → accumulators (register g of lane l: cout (g&3) + 8(g>>2) + 4hh of fragment f)
+            const float* bs = reinterpret_cast<const float*>(smem + tk::BIAS_OFF + bslot * 256);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                f32x16 b0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 q = *reinterpret_cast<const f32x4*>(bs + f * 32 + 8 * j + 4 * hh);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) b0[4 * j + e] = q[e];
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r][f] = b0;
+            }
+        }
+        // ---- the chunk after this one: may its DMA be issued now? ----
+        const bool last = ch + 1 == nch;
+        bool issue_next = false, checks = false, nx_checks = false;
+        if (!last) {
+            issue_next = true;
+            checks = ch + 1 >= first_new && !dep_ok;
+        } else if (nx.exists) {
+            // the next item's chunk 0 needs the wait when its previous layer wrote it; when the
+            // tile computed now is in its neighbourhood, it cannot be staged before this tile's
+            // stores land (deferred to the top of the next item)
+            const bool needs = nx.first_new == 0 && nx.L > 0;
+            issue_next = !(needs && nx.self_dep);
+            checks = nx_checks = issue_next && needs;
+        }
+        // early poll for the NEXT item's refill (its answer lands by that item's top-of-item
+        // vmcnt): the dependency of own chunk ch + 2, or of the next tile's chunk 0
+        const bool poll_own = ch + 2 < nch && ch + 2 == first_new && !dep_ok;
+        const bool poll_nx = ch + 2 == nch && nx.exists && nx.first_new == 0 && nx.L > 0 && !nx.self_dep;
+
+        const char* sb = smem + slot * tk::SLOT;
+        bf16x8 fb[2][TN][NF], fa[2][NA];
+        auto read_one = [&](int dx, int idx, int set) {
+            if (idx < TN * NF) {
+                const int dyi = idx / NF, f = idx % NF;
+                fb[set][dyi][f] = lds_read16(sb + a_w + ((dyi * 3 + dx) * CT * 2 + f * 64) * 16);
+            } else {
+                const int ia = idx - TN * NF;
+                fa[set][ia] = lds_read16(sb + a_h[dx] + ia * tk::HC * 32);
+            }
+        };
+        // step 0's fragments in order of first use (dy-major MFMA order below)
+        auto read_fb = [&](int dx, int dyi, int set) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f) read_one(dx, dyi * NF + f, set);
+        };
+        read_fb(0, 0, 0);
+#pragma unroll
+        for (int ia = 0; ia < R; ++ia) read_one(0, TN * NF + ia, 0);
+        read_fb(0, 1, 0);
+        read_one(0, TN * NF + R, 0);
+        read_fb(0, 2, 0);
+        read_one(0, TN * NF + R + 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- refill: the next chunk (own, or the next item's first) into the other slot ----
+        if (issue_next) {
+            bool go = true;
+            if (checks) {
+                const int nbq = nx_checks ? nb_of(nx.t, c.nbx, c.nby) : nb_of(t, c.nbx, c.nby);
+                const unsigned needq = nx_checks ? c.gen * 1024u + (unsigned)nx.L : need;
+                const unsigned v = st.polled ? st.pollv : poll_load(c.state + 4, nbq);
+                go = __all(nbq < 0 || (int)(v - needq) >= 0);
+                if (go && c.acquire) acquire_fence();
+            }
+            if (go) {
+                if (!last) stage_chunk(c, me, ch + 1, slot ^ 1, false, 0);
+                else stage_chunk(c, nx.src, 0, slot ^ 1, true, bslot ^ 1);
+                if (checks && !last) dep_ok = true;
+                if (checks && last) st.dep_next = true;
+            }
+            st.staged = go;
+            st.mixed = checks;
+        } else {
+            st.staged = !(last && nx.exists);  // nothing follows: nothing to stage
+            st.mixed = false;
+        }
+        st.polled = false;
+        if (poll_own || poll_nx) {
+            const int nbq = poll_nx ? nb_of(nx.t, c.nbx, c.nby) : nb_of(t, c.nbx, c.nby);
+            st.pollv = poll_load(c.state + 4, nbq);
+            st.polled = true;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- MFMAs: 3 steps (dx), each in kernel-row-major order (dy, then output row r):
+        // every accumulator still sees dy 0, 1, 2 in that order (conv3x3.hip's input-row-major
+        // loop gives each accumulator the same sequence, so the bits agree).  The next step's
+        // fragment of kernel row dy is read right after that row's last MFMA here, and its
+        // input row ia right after the current one's last use — one live register set plus
+        // the rows in flight, each read ~16 MFMAs before it is needed. ----
+#pragma unroll
+        for (int stp = 0; stp < 3; ++stp) {
+            const int cur = stp & 1;
+#pragma unroll
+            for (int dyi = 0; dyi < TN; ++dyi) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) {
+                        if (trunk_abl() & 2) asm volatile("" ::"v"(fb[cur][dyi][f]), "v"(fa[cur][r + dyi]));
+                        else acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][r + dyi], acc[r][f]);
+                    }
+                    if constexpr (NF == 2) {
+                        // residual fold: + x/s1 on the centre pixels of row r (dx = 1, dy = 1),
+                        // between the row's dy = 1 and dy = 2 contributions
+                        if (dyi == 1 && stp == 1 && fold && ch < 4) {
+                            const bf16x8 a = fold_a_bits(rec_idv(rec), ch & 1);
+                            if (ch < 2) acc[r][0] = mfma32(a, fa[cur][r + 1], acc[r][0]);
+                            else acc[r][1] = mfma32(a, fa[cur][r + 1], acc[r][1]);
+                        }
+                    }
+                    // input row ia = r + dyi is last used here when dyi == min(2, ia)
+                    if (stp + 1 < 3 && (dyi == 2 || r == 0)) read_one(stp + 1, TN * NF + r + dyi, cur ^ 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (stp + 1 < 3) {
+                    read_fb(stp + 1, dyi, cur ^ 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+    }
+    trunk_stamp(L, t, c.ntiles, 2);
+
+    // the neighbourhood must be done with layer L-1 before this tile's outputs land (a layer
+    // that reads nothing its predecessor wrote never waited above)
+    if (!dep_ok && first_new != tk::NEED_NONE) dep_wait(c.state, nb_of(t, c.nbx, c.nby), need, c.gen);
+
+    // ---- epilogue: straight from the accumulators, write-through (sc1) stores ----
+    {
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+        const int xx = x0 + l31;
+        const auto yr = __builtin_amdgcn_make_buffer_rsrc((char*)(uintptr_t)rec.y, (short)0, 0x7fffffff, 0x00020000);
+        const bool has_r2 = NF == 2 && rec.r2 != 0;
+        const auto rr = __builtin_amdgcn_make_buffer_rsrc((char*)(uintptr_t)rec.r2, (short)0, 0x7fffffff, 0x00020000);
+        const float slope = rec.slope, s1 = rec.s1, s2 = rec.s2;
+        const bool scale2 = s2 != 1.f;
+        const uint32_t plane_px = (uint32_t)(c.hp * c.wp);
+        // channel-plane offsets (in pixels) of this lane's first y / r2 plane
+        const uint32_t ypl = (uint32_t)(img * c.cs16 + rec_yp(rec)) * plane_px;
+        const uint32_t r2pl = (uint32_t)(img * c.cs16 + rec_r2p(rec)) * plane_px;
+        bf16x8 q2[R][NF][2];
+        if (has_r2) {  // RRDB residual: every load of the tile issued before any use
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t pix = (uint32_t)((y0 + wave * R + r + c.pad) * c.wp + xx + c.pad);
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int blk = 0; blk < 2; ++blk) {
+                        const int co = f * 32 + 16 * blk + 8 * hh;
+                        const uint32_t off = (r2pl + (uint32_t)(co >> 4) * plane_px + pix) * 32 + 16 * hh;
+                        q2[r][f][blk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 16));
+                    }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int yy = y0 + wave * R + r;
+            const bool valid = yy < c.h && xx < c.w;
+            const uint32_t pix = (uint32_t)((yy + c.pad) * c.wp + xx + c.pad);
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                float v[16];
+#pragma unroll
+                for (int g = 0; g < 16; ++g) v[g] = acc[r][f][g];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    swap_halves(v[k], v[4 + k]);
+                    swap_halves(v[8 + k], v[12 + k]);
+                }
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    float* u = v + 8 * blk;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
+                        if (fold) u[e] = u[e] * s1;
+                        if (has_r2) {
+                            u[e] = u[e] * s2 + (float)q2[r][f][blk][e];
+                        } else {
+                            if (scale2) u[e] *= s2;
+                        }
+                        if (!valid) u[e] = 0.f;
+                    }
+                    const int co = f * 32 + 16 * blk + 8 * hh;
+                    const uint32_t off = (ypl + (uint32_t)(co >> 4) * plane_px + pix) * 32 + 16 * hh;
+                    bf16x8 tq;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) tq[e] = (__bf16)u[e];
+                    if (!(trunk_abl() & 4))
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tq), yr, off, 0, 16);
+                }
+            }
+        }
+    }
+    trunk_stamp(L, t, c.ntiles, 3);
+    st.pend_t = t;
+    st.pend_v = c.gen * 1024u + (unsigned)(L + 1);
+    ++st.tseq;
+}
+
+__global__ __launch_bounds__(tk::NT, 2) void trunk_kernel(TrunkArgs a) {
+    TrunkCtx c;
+    c.state = a.state;
+    c.acquire = a.acquire;
+    c.gen = __hip_atomic_load(a.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const_geo& g = *(const_geo*)(uintptr_t)(a.state + a.rec_off - 16);
+    const_rec* recs = (const_rec*)(uintptr_t)(a.state + a.rec_off);
+    if (g.err != 0) {  // the prep kernel refused the layer table: give up loudly
+        if (threadIdx.x == 0) __hip_atomic_store(a.state + 1, c.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    c.hp = g.hp;
+    c.wp = g.wp;
+    c.cs16 = g.cs16;
+    c.pad = g.pad;
+    c.h = g.h;
+    c.w = g.w;
+    c.nbx = g.nbx;
+    c.nby = g.nby;
+    c.ntiles = g.ntiles;
+    c.pstride = (uint32_t)(c.hp * c.wp * 32);
+    {
+        const int wave = wave_id(), lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < tk::HPW; ++k) c.hoff[k] = halo_piece_off(wave + tk::WM * k, lane, c.wp);
+    }
+    const int G = gridDim.x, b = blockIdx.x;
+    Stream st;
+    st.item = 0;
+    st.tseq = 0;
+    st.pend_t = -1;
+    st.pend_v = 0;
+    st.mixed = false;
+    st.polled = false;
+    st.pollv = 0;
+    st.dep_next = false;
+    st.staged = true;
+    if (b < c.ntiles) {
+        stage_chunk(c, src_of(c, recs[0], b), 0, 0, true, 0);  // layer 0 reads the trunk input only
+        for (int L = 0; L < a.nl; ++L) {
+            const_rec& rec = recs[L];
+            for (int t = b; t < c.ntiles; t += G) {
+                Next nx;
+                nx.exists = true;
+                if (t + G < c.ntiles) {
+                    nx.L = L;
+                    nx.t = t + G;
+                } else if (L + 1 < a.nl) {
+                    nx.L = L + 1;
+                    nx.t = b;
+                } else {
+                    nx.exists = false;
+                    nx.L = L;
+                    nx.t = t;
+                }
+                const_rec& nrec = recs[nx.L];
+                nx.src = src_of(c, nrec, nx.t);
+                nx.first_new = rec_first_new(nrec);
+                {
+                    const int bx = t % c.nbx, tq = t / c.nbx, by = tq % c.nby, im = tq / c.nby;
+                    const int bx2 = nx.t % c.nbx, nq = nx.t / c.nbx, by2 = nq % c.nby, im2 = nq / c.nby;
+                    nx.self_dep = im == im2 && abs(bx - bx2) <= 1 && abs(by - by2) <= 1;
+                }
+                if (rec_kind(rec) == 0) run_tile<1>(c, st, rec, L, t, nx);
+                else run_tile<2>(c, st, rec, L, t, nx);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && st.pend_t >= 0)
+        __hip_atomic_store(c.state + 4 + st.pend_t, st.pend_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid: every workgroup must be resident at once (tiles wait on other workgroups' tiles), so
+// the grid is min(tiles, resident workgroups) with residency from the occupancy API (capped at
+// the 2 per CU the kernel is built for); ISR_ERR when that is below one workgroup per CU.
+int trunk_launch(const isr_chain_desc* cd, hipStream_t s) {
+    if (cd->ha % tk::TH || cd->wa % tk::TW || cd->nl < 1 || cd->nl > 1024) return -2;
+    const int nbx = cd->wa / tk::TW, nby = cd->ha / tk::TH;
+    const long long ntiles = (long long)cd->n * nbx * nby;
+    if (ntiles <= 0 || ntiles > (1 << 24)) return -2;
+    static thread_local int cached_dev = -1, cached_per_cu = 0, cached_cus = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (dev != cached_dev) {
+        (void)hipFuncSetAttribute((const void*)trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, tk::LDS);
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trunk_kernel, tk::NT, tk::LDS) !=
+            hipSuccess)
+            return -1;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return -1;
+        cached_dev = dev;
+        cached_per_cu = per_cu < 2 ? per_cu : 2;
+        cached_cus = cus;
+    }
+#ifdef ISR_TUNING
+    if (g_trunk_per_cu > 0 && g_trunk_per_cu < cached_per_cu) cached_per_cu = g_trunk_per_cu;
+#endif
+    if (cached_per_cu < 1) return -4;
+    const long long slots = (long long)cached_per_cu * cached_cus;
+    const int grid = (int)(ntiles < slots ? ntiles : slots);
+    const int rec_off = (int)trunk_rec_off((int)ntiles);
+    hipLaunchKernelGGL(trunk_prep_kernel, dim3(1), dim3(1024), 16, s, cd->layers, cd->kinds, cd->nl, cd->n, cd->ha,
+                       cd->wa, cd->state);
+    TrunkArgs a;
+    a.state = cd->state;
+    a.rec_off = rec_off;
+    a.nl = cd->nl;
+    a.acquire = cd->acquire;
+    hipLaunchKernelGGL(trunk_kernel, dim3(grid), dim3(tk::NT), tk::LDS, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+#ifdef ISR_TUNING
+int trunk_knobs_set(const int* k) {
+    g_trunk_per_cu = k[1];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
+}
+int trunk_stamps_set(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+#else
+int trunk_knobs_set(const int*) { return -2; }
+int trunk_stamps_set(void*) { return -2; }
+#endif
+
+}  // namespace isr

@@ -244,9 +244,10 @@ class ConvChain:
     """Device-side layer table + state for isr_conv_chain over a run of RDB convs
     (growth convs: kind 0; 192→64 final convs: kind 1) sharing one tile grid."""
 
-    def __init__(self, descs, grid: ActBuffer, device, acquire: bool = False):
+    def __init__(self, descs, grid: ActBuffer, device, acquire: bool = False, variant: int | None = None):
         lib = ops._lib.load()
         kinds = []
+        g = descs[0].x
         for d in descs:
             ops.check(lib.isr_conv3x3_check(ctypes.byref(d)), "chain layer")
             if d.cout == 32:
@@ -259,8 +260,19 @@ class ConvChain:
                 raise ValueError("conv chain: plain 3x3 layers only")
             if (d.n, d.ha, d.wa) != (grid.n, grid.ha, grid.wa):
                 raise ValueError("conv chain: every layer must share the tile grid")
+            # the trunk kernel's layer records (trunk.hip) share one view geometry and fold r1
+            views = [d.x, d.y] + ([d.r2] if d.r2.data else [])
+            if any((v.hp, v.wp, v.cs, v.pad) != (g.hp, g.wp, g.cs, g.pad) for v in views) or not d.bias:
+                raise ValueError("conv chain: every layer must share one buffer geometry and carry a bias")
+            if d.r1.data and not (d.r1.data == d.x.data and d.r1.coff == d.x.coff and d.r1_cn == 0
+                                  and d.slope == 1.0 and _bf16_exact(1.0 / d.s1)):
+                raise ValueError("conv chain: r1 must be the layer's own input (identity activation, "
+                                 "1/s1 exact in bf16)")
+            if d.r2.data and not d.r1.data:
+                raise ValueError("conv chain: r2 without r1")
         if grid.t.numel() * 2 >= 2 ** 31:
             raise ValueError("conv chain: activation buffers must stay below 2 GiB (buffer-descriptor window)")
+        self.variant = CHAIN_VARIANT if variant is None else variant
         raw = b"".join(bytes(d) for d in descs)
         self._table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
         self._kinds = torch.tensor(kinds, dtype=torch.int32, device=device)
@@ -268,8 +280,12 @@ class ConvChain:
         self.state = torch.zeros(words, dtype=torch.int32, device=device)
         self.desc = ops._lib.IsrChainDesc(self._table.data_ptr(), self._kinds.data_ptr(), len(descs), grid.n,
                                           grid.ha, grid.wa, self.state.data_ptr(), int(acquire))
-        self.fn = lib.isr_conv_chain
         self.nl = len(descs)
+        if self.variant == 0:
+            self.fn = lib.isr_conv_chain
+        else:
+            fv, var = lib.isr_conv_chain_variant, self.variant
+            self.fn = lambda d, s: fv(d, var, s)
 
     def failed(self) -> bool:
         """True when a dependency wait gave up in the last launch (results invalid)."""
@@ -366,7 +382,17 @@ def _sleep_cycles_per_us() -> float:
 # relies on the sc1 (L1-bypassing) activation loads alone (-1.5 % time).
 import os as _os
 CHAIN_DEFAULT = _os.environ.get("ISR_CHAIN", "1") == "1"
-CHAIN_ACQUIRE = _os.environ.get("ISR_CHAIN_ACQUIRE", "1") == "1"
+# The hand-off reads are sc1 LDS-DMA loads, which bypass L1; an agent-scope acquire only
+# invalidates L1, so it adds nothing to them and costs ~1 ms per forward on the trunk kernel
+# (per-wave fences).  Both modes are bitwise-tested (tests/test_gpu_chain.py).
+CHAIN_ACQUIRE = _os.environ.get("ISR_CHAIN_ACQUIRE", "0") == "1"
+# isr_conv_chain_variant: 0 = trunk.hip (production), 1 = the round-2 per-tile chain kernel
+CHAIN_VARIANT = int(_os.environ.get("ISR_CHAIN_VARIANT", "0"))
+
+
+def _bf16_exact(v: float) -> bool:
+    t = torch.tensor([v], dtype=torch.float32)
+    return bool(t.to(torch.bfloat16).to(torch.float32).item() == t.item())
 
 # Batches of >= 2 (even) are split over this many HIP streams by default: two
 # half-batch launch lists run concurrently, so one stream's kernel tail, prologue

@@ -356,6 +356,22 @@ typedef struct isr_chain_desc {
 } isr_chain_desc;
 size_t isr_conv_chain_state_words(int32_t n, int32_t ha, int32_t wa);
 int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
+/* The same with the kernel chosen: 0 = production (trunk.hip: one continuous K-chunk stream per
+ * workgroup across its (layer, tile) items, waits only before the chunks the previous layer
+ * wrote, the RDB residual folded into the MFMAs; needs every view to share (hp, wp, cs, pad),
+ * a bias, cin >= 64, r1 (if any) == the layer's own input with slope 1 and 1/s1 exact in bf16 —
+ * a table that breaks this makes the launch give up: state[1] == state[0]); 1 = the round-2
+ * kernel (conv3x3.hip: one independent conv tile per (layer, tile)).  Both produce the outputs
+ * of the per-layer isr_conv3x3_fwd calls bit for bit. */
+int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
+/* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
+ * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,
+ * wait met; s_memrealtime ticks, 100 MHz); NULL stops. */
+int isr_tuning_trunk_stamps(void* buf);
+/* Tuning builds only: ablations of later production chain launches (timing only, outputs wrong):
+ * bit 1 = no halo LDS-DMA after the first chunk, 2 = no MFMAs, 4 = no epilogue stores;
+ * per_cu > 0 caps the resident workgroups per CU (the grid). */
+int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k3);
 
 int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s);
 int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);

@@ -25,12 +25,20 @@ def _gw(blocks, scale=4, enchant=False, seed=0):
     return engine.pack_generator({k: v.to(DEV) for k, v in sd.items()}, enchant=enchant, device=DEV)
 
 
-def _run(gw, xs, chain, acquire=False):
+def _run(gw, xs, chain, acquire=False, variant=0):
     """One plan, one forward per input in `xs` (different inputs back to back: a stale
     hand-off read would return the previous input's activations and show up)."""
     x0 = xs[0]
-    plan = engine.GeneratorPlan(gw, x0.shape[0], x0.shape[2], x0.shape[3], x0.device, False, False,
-                                (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), chain=chain, chain_acquire=acquire)
+    old = engine.CHAIN_VARIANT
+    engine.CHAIN_VARIANT = variant
+    try:
+        plan = engine.GeneratorPlan(gw, x0.shape[0], x0.shape[2], x0.shape[3], x0.device, False, False,
+                                    (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), chain=chain,
+                                    chain_acquire=acquire)
+    finally:
+        engine.CHAIN_VARIANT = old
+    if chain:
+        assert plan.chain is not None and plan.chain.variant == variant
     outs = []
     for x in xs:
         out = torch.empty(plan.out_shape, device=DEV)
@@ -46,14 +54,20 @@ def _inputs(n, h, w, k, seed):
     return [normalize(synth_lr_batch(n, h, w, seed=seed + i, scale=4)[0]).to(DEV).contiguous() for i in range(k)]
 
 
-@pytest.mark.parametrize("n,h,w,blocks", [(2, 36, 52, 2), (1, 128, 128, 1), (16, 128, 128, 16), (4, 256, 256, 2)])
+# (4, 512, 512) = 2,048 tiles and (1, 540, 960) = 1,020 ragged tiles: more tiles than the 512
+# resident workgroups of a 256-CU chip, so every workgroup walks several tiles per layer (the
+# video and 4K-still geometry)
+@pytest.mark.parametrize("n,h,w,blocks", [(2, 36, 52, 2), (1, 128, 128, 1), (16, 128, 128, 16), (4, 256, 256, 2),
+                                          (4, 512, 512, 1), (1, 540, 960, 1)])
 def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks):
     gw = _gw(blocks)
     xs = _inputs(n, h, w, 3, seed=3)
     refs = _run(gw, xs, chain=False)
-    for acquire in (False, True):
-        for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire), refs):
-            assert torch.equal(out, ref), f"chain (acquire={acquire}) differs: max {(out - ref).abs().max().item()}"
+    for variant in (0, 1):
+        for acquire in (False, True):
+            for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire, variant=variant), refs):
+                assert torch.equal(out, ref), \
+                    f"chain variant {variant} (acquire={acquire}) differs: max {(out - ref).abs().max().item()}"
 
 
 def test_chain_repeated_stress_eresnet():
@@ -66,6 +80,22 @@ def test_chain_repeated_stress_eresnet():
     for _ in range(5):
         for out, ref in zip(_run(gw, xs, chain=True), refs):
             assert torch.equal(out, ref)
+
+
+def test_chain_rejects_a_bad_layer_table_loudly():
+    """The trunk kernel's prep pass refuses a layer table its records cannot express (here: a
+    growth layer whose kind says 'final'): the launch gives up (state[1] == state[0]) instead of
+    computing garbage silently, and the product-path check raises."""
+    gw = _gw(1)
+    x = _inputs(2, 32, 32, 1, seed=1)[0]
+    plan = engine.GeneratorPlan(gw, 2, 32, 32, x.device, False, False, (0.485, 0.456, 0.406),
+                                (0.229, 0.224, 0.225), chain=True)
+    assert plan.chain.variant == 0
+    plan.chain._kinds[0] = 1  # growth conv (cout 32) declared as an RDB final conv
+    out = torch.empty(plan.out_shape, device=DEV)
+    plan.run(x, out)
+    torch.cuda.synchronize()
+    assert plan.chain.failed()
 
 
 def test_chain_poll_reports_a_give_up():

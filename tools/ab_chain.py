@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Whole-generator A/B of the persistent RRDB-trunk kernel (isr_conv_chain) against
 per-conv launches, every config HIP-graph captured, interleaved rounds in one process
-(cdna_hip_programming.md §5.4 rule 24).  Configs "S:C:A" = streams S, chain C (0/1),
-acquire A (0/1).  Outputs must be bit-identical.
+(cdna_hip_programming.md §5.4 rule 24).  Configs "S:C:A[:V]" = streams S, chain C (0/1),
+acquire A (0/1), chain kernel variant V (isr_conv_chain_variant: 0 trunk.hip, 1 round-2).  Outputs must be bit-identical.
 usage: python tools/ab_chain.py --configs 2:0:0,1:0:0,1:1:0,1:1:1,2:1:0
 """
 from __future__ import annotations
@@ -37,7 +37,9 @@ def main():
     mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
     runs = {}
     for c in args.configs.split(","):
-        s_, ch, acq = (int(v) for v in c.split(":"))
+        f = [int(v) for v in c.split(":")]
+        s_, ch, acq = f[:3]
+        engine.CHAIN_VARIANT = f[3] if len(f) > 3 else 0
         n, hw = args.batch, args.lr_size
         if s_ > 1:
             plan = engine.SplitGeneratorPlan(gw, n, hw, hw, dev, False, False, mean, std, splits=s_, chain=bool(ch))
