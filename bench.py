@@ -4,8 +4,10 @@
 Workload: ResNet(num_block_resnet=16, add_rate=0.2, scaleRate=4) — the reference's
 RRDB generator (utils/models.py:592-618) — bf16 on the HIP kernels, 16 synthetic
 128x128 LR tiles per GPU → 16 x 512x512 HR, inputs resident in HBM.  One step =
-one generator forward over the batch, split over 2 HIP streams (8 tiles each,
-engine.SplitGeneratorPlan; --streams 1 for the single-stream plan).  Multi-GPU: one process per GPU, each
+one generator forward over the batch on one HIP stream: head9x9, the whole RRDB trunk as
+ONE persistent launch (isr_conv_chain → trunk.hip), conv1, two Scalers, tail9x9
+(--streams k > 1 selects the per-conv split plan, engine.SplitGeneratorPlan, for A/B
+only).  Multi-GPU: one process per GPU, each
 rank runs its own 16 tiles (tiles are independent: weak scaling, no
 collective on the data path; only the timing uses a MAX all-reduce).
 
@@ -75,7 +77,7 @@ def parse():
     ap.add_argument("--scale", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r02")
+    ap.add_argument("--round", default="r03")
     ap.add_argument("--no-graph", action="store_true", help="eager launch loop instead of the HIP graph")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N>1 (nccl = RCCL)")
     ap.add_argument("--streams", type=int, default=None,
@@ -183,9 +185,7 @@ def main():
         elapsed = tt.item()
 
     ms = elapsed / args.steps * 1e3
-    for p in (plan.subs if n_streams > 1 else [plan]):  # a persistent-chain wait that gave up voids the run
-        if p.chain is not None and p.chain.failed():
-            raise engine.ChainFailed("bench: a chain dependency wait gave up during the timed steps")
+    plan.verify()  # a persistent-chain give-up in any timed step (sticky count) voids the run: raises
     hr_px = n * (hw * S) * (hw * S)
     mpix_s = world * hr_px * args.steps / elapsed / 1e6
     # Per-kernel roofline, after the timed region.  The production forward's dominant kernel
@@ -205,7 +205,7 @@ def main():
         trunk_flops = args.blocks * 3 * (sum(2.0 * 9 * (64 + 32 * k) * 32 for k in range(4))
                                          + 2.0 * 9 * 192 * 64) * npx
         c_gbs = trunk_bytes / (c_ms * 1e-3) / 1e9
-        kernels["chain"] = {"bound": "hbm", "kernel": "conv_chain_kernel (RRDB trunk: 240 convs, one persistent launch)",
+        kernels["chain"] = {"bound": "hbm", "kernel": "trunk_kernel (trunk.hip: the RRDB trunk, 240 convs, one persistent launch)",
                             "achieved": round(c_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(c_gbs / HBM_PEAK_GBS, 4), "traffic": traffic.get("chain"),
                             "bytes_per_launch": trunk_bytes, "flops_per_launch": trunk_flops,

@@ -16,9 +16,10 @@ int tail_stamps_set(void* p);
 size_t conv_chain_state_words(int n, int ha, int wa);
 int conv_chain(const isr_chain_desc* c, hipStream_t s);
 size_t trunk_state_words(int n, int ha, int wa);
-int trunk_launch(const isr_chain_desc* c, hipStream_t s);
+int trunk_launch(const isr_chain_desc* c, hipStream_t s, int form);
 int trunk_stamps_set(void* p);
 int trunk_knobs_set(const int* k);
+int trunk_item_stamps_set(void* p);
 size_t conv3x3_packed_bytes(int cout, int cin);
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
 int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s);
@@ -235,8 +236,8 @@ int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_
         return fail(ISR_ERR_BAD_DESC, "conv chain: null layers / kinds / state or nl not in [1, 1024]");
     if (c->n <= 0 || c->ha <= 0 || c->wa <= 0 || c->ha % 16 || c->wa % 32)
         return fail(ISR_ERR_BAD_DESC, "conv chain: bad grid n=%d ha=%d wa=%d", c->n, c->ha, c->wa);
-    if (variant == 0) {
-        const int rc = isr::trunk_launch(c, (hipStream_t)s);
+    if (variant == 0 || variant == 2) {
+        const int rc = isr::trunk_launch(c, (hipStream_t)s, variant == 2 ? 1 : 0);
         if (rc == -4) return fail(ISR_ERR_LAUNCH, "conv chain: the occupancy query admits no workgroup per CU");
         if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "conv chain: unsupported grid or layer count");
         return launched(rc, "conv chain");
@@ -252,6 +253,12 @@ int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k
     const int rc = isr::trunk_knobs_set(k);
     if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "trunk knobs: library built without -DISR_TUNING");
     return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "trunk knobs: hipMemcpyToSymbol failed");
+}
+
+int isr_tuning_trunk_item_stamps(void* buf) {
+    const int rc = isr::trunk_item_stamps_set(buf);
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "trunk item stamps: library built without -DISR_TUNING");
+    return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "trunk item stamps: hipMemcpyToSymbol failed");
 }
 
 int isr_tuning_trunk_stamps(void* buf) {

@@ -839,7 +839,10 @@ __device__ __forceinline__ void chain_wait(const ChainArgs& a, int t, unsigned n
                 __hip_atomic_load(a.state + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen)
                 break;
             if (spins > (1u << 18)) {
-                if (lane == 0) __hip_atomic_store(a.state + 1, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) {
+                    __hip_atomic_store(a.state + 1, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(a.state + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -954,8 +957,11 @@ static int launch_chain(const isr_chain_desc* c, hipStream_t s) {
     hipLaunchKernelGGL(chain_bump_kernel, dim3(1), dim3(64), 0, s, c->state);
     auto kern = conv_chain_kernel<CG, CF, WM_>;
     constexpr int lds = CG::LDS > CF::LDS ? CG::LDS : CF::LDS;
-    constexpr int per_cu = 163840 / lds < 2 ? 163840 / lds : 2;  // the kernel's occupancy (<= 2 by registers)
     lds_limit((const void*)kern, lds);
+    int per_cu = 0;  // residency from the occupancy API (registers, LDS), capped at the 2 it is built for
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, CG::NT, lds) != hipSuccess) return -1;
+    per_cu = per_cu < 2 ? per_cu : 2;
+    if (per_cu < 1) return -1;
     const int slots = per_cu * cu_count();  // every workgroup resident
     const int grid = a.ntiles < slots ? a.ntiles : slots;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(CG::NT), lds, s, a);

@@ -445,9 +445,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(isr_bn_desc d) {
 // dz = gscale * a * (g - sum(g)/N - xhat * sum(g*xhat)/N), in place over y; dgamma/dbeta
 template <typename I>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(isr_bn_desc d) {
-    // dz = gs*gamma*istd * (g - mean(g) - xhat * mean(g*xhat)) = A*g + B*z + C per channel, with
-    // A, B, C computed once per block in LDS (the element loop had two fp64 divides per value)
-    __shared__ float ca[BN_MAX_C], cb[BN_MAX_C], cc[BN_MAX_C];
+    // dz = gs*gamma*istd * (g - mean(g) - xhat * mean(g*xhat)) = A*(g - mg) - K*(z - mean) per
+    // channel, with A, mg, K = A*istd*mean(g*xhat) and the mean computed once per block in LDS (the
+    // element loop had two fp64 divides per value).  The subtraction z - mean is kept explicit: a
+    // folded B*z + C form cancels in fp32 when |mean| >> std.
+    __shared__ float ca[BN_MAX_C], cb[BN_MAX_C], cc[BN_MAX_C], cm[BN_MAX_C];
     const int cg = d.c / 8;
     const I total = (I)((size_t)d.n * d.ha * d.wa * cg);
     const double cnt = (double)d.n * d.h * d.w;
@@ -456,8 +458,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(isr_bn_desc d) {
         const float mg = (float)(d.acc[c] / cnt), mgx = (float)(d.acc[d.c + c] / cnt);
         const float A = d.gscale * d.gamma[c] * istd;
         ca[c] = A;
-        cb[c] = -A * istd * mgx;
-        cc[c] = A * (mean * istd * mgx - mg);
+        cb[c] = A * istd * mgx;
+        cc[c] = mg;
+        cm[c] = mean;
     }
     __syncthreads();
     if (blockIdx.x == 0) {
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(isr_bn_desc d) {
             load8_bf16(view_at(d.z, img, y, x, c), z);
             load8_bf16(view_at(d.y, img, y, x, c), g);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = ca[c + k] * g[k] + (cb[c + k] * z[k] + cc[c + k]);
+            for (int k = 0; k < 8; ++k) v[k] = ca[c + k] * (g[k] - cc[c + k]) - cb[c + k] * (z[k] - cm[c + k]);
         }
         store8_bf16(view_at(d.dz.data ? d.dz : d.y, img, y, x, c), v);
     }

@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <mutex>
+#include <atomic>
 #include <set>
 #include <utility>
 
@@ -194,31 +194,30 @@ __device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int 
     if (e.y2.data) store8_bf16(view_at(e.y2, img, yy, xx, co), v);
 }
 
-// Raise `kern`'s dynamic-LDS limit to `bytes` once per (kernel, device).  The
-// library is called from the Python thread (forward) and from autograd's device
-// thread (backward), and one process may drive several devices, so the
-// bookkeeping is per device and mutex-protected.
+// Raise `kern`'s dynamic-LDS limit to `bytes` once per (kernel, device, host thread).  The
+// library is called from the Python thread (forward) and from autograd's device thread
+// (backward), and one process may drive several devices; a thread-local record keeps the launch
+// path free of locks (hipFuncSetAttribute is idempotent, so each thread setting it once is fine).
 inline void lds_limit(const void* kern, int bytes) {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    static std::mutex mu;
-    static std::set<std::pair<const void*, int>> done;
-    std::lock_guard<std::mutex> lock(mu);
+    static thread_local std::set<std::pair<const void*, int>> done;
     if (done.insert({kern, dev}).second)
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-// Compute units of the current device (cached per device).
+// Compute units of the current device (cached per device, lock-free after the first query).
 inline int cu_count() {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    static std::mutex mu;
-    static int cache[64] = {0};
-    std::lock_guard<std::mutex> lock(mu);
-    int& c = cache[dev & 63];
-    if (c <= 0 && (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0))
-        c = 256;
-    return c;
+    static std::atomic<int> cache[64];
+    std::atomic<int>& c = cache[dev & 63];
+    int v = c.load(std::memory_order_relaxed);
+    if (v <= 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        c.store(v, std::memory_order_relaxed);
+    }
+    return v;
 }
 
 }  // namespace isr

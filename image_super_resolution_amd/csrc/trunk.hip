@@ -30,20 +30,11 @@
 namespace isr {
 
 namespace tk {
-constexpr int R = 4;            // output rows per wave
-constexpr int WM = 4;           // waves per workgroup
-constexpr int NT = 64 * WM;
-constexpr int TH = R * WM;      // 16-row tile
+constexpr int TH = 16;          // tile rows (R x WM of a build)
 constexpr int TW = 32;
 constexpr int HR = TH + 2, HC = TW + 2, HQ = HR * HC;  // 18 x 34 halo pixels
 constexpr int HP = (HQ + 31) / 32;                      // 20 halo pieces (1 KB) per chunk
-constexpr int HPW = HP / WM;                            // 5 per wave
-static_assert(HP % WM == 0, "halo pieces per wave");
 constexpr int WPG = 9, WPF = 18;                        // weight pieces per chunk: 32 / 64 couts
-constexpr int SLOT = (HP + WPF) * 1024;                 // 38 KB ring slot
-constexpr int BIAS_OFF = 2 * SLOT;                      // 2 x 256 B bias slots
-constexpr int FLAG_OFF = BIAS_OFF + 512;                // per-wave "refill deferred" words
-constexpr int LDS = FLAG_OFF + 16;
 constexpr int NEED_NONE = 255;
 }  // namespace tk
 
@@ -190,15 +181,34 @@ __device__ __forceinline__ bool rec_fold(const_rec_t& r) { return ((r.deps >> 8)
 __device__ __forceinline__ uint32_t rec_idv(const_rec_t& r) { return r.deps >> 16; }
 
 // Tuning builds: ablation knobs (timing only, outputs wrong): bit 1 = no halo LDS-DMA after the
-// first item, 2 = no MFMAs (operands kept live), 4 = no epilogue stores; [1] = workgroups per CU
-// (host side, 0 = occupancy).
+// first item, 4 = no epilogue stores; [1] = workgroups per CU (host side, 0 = occupancy).  (An
+// MFMA ablation branch inside the step loop would cut the MFMA/read schedule into blocks.)
 #ifdef ISR_TUNING
 __device__ int g_trunk_knobs[4];
 static int g_trunk_per_cu = 0;
-__device__ __forceinline__ int trunk_abl() { return g_trunk_knobs[0]; }
+__device__ __forceinline__ int trunk_abl_load() { return __builtin_amdgcn_readfirstlane(g_trunk_knobs[0]); }
 #else
-__device__ __forceinline__ int trunk_abl() { return 0; }
+__device__ __forceinline__ int trunk_abl_load() { return 0; }
 #endif
+
+// Tuning builds: per-item cycle stamps (s_memtime) for layers 77 (growth2, 8 chunks) and 79 (final,
+// 12 chunks) of tile 0 of each workgroup's first tile: lane 0 of waves 0 and WM/2, 8 slots per item:
+// [0] item top, [1] own DMA landed, [2] barrier passed, [3] refill issued, [4] MFMAs issued.
+#ifdef ISR_TUNING
+__device__ unsigned long long* g_item_stamps;
+#endif
+__device__ __forceinline__ void item_stamp(int L, int first_tile, int ch, int slot, int wm) {
+#ifdef ISR_TUNING
+    unsigned long long* p = g_item_stamps;
+    const int w = wave_id();
+    if (p != nullptr && first_tile && (threadIdx.x & 63) == 0 && (w == 0 || w == wm / 2) && (L == 77 || L == 79)) {
+        const unsigned long long v = __builtin_amdgcn_s_memtime();
+        p[((((size_t)blockIdx.x * 2 + (L == 79)) * 16 + ch) * 2 + (w != 0)) * 8 + slot] = v;
+    }
+#else
+    (void)L, (void)first_tile, (void)ch, (void)slot, (void)wm;
+#endif
+}
 
 struct TrunkArgs {
     unsigned* state;
@@ -242,7 +252,10 @@ __device__ __forceinline__ void dep_wait(unsigned* state, int nb, unsigned need,
         if ((spins & 255) == 255 && __hip_atomic_load(state + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen)
             break;
         if (spins > (1u << 18)) {
-            if ((threadIdx.x & 63) == 0) __hip_atomic_store(state + 1, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((threadIdx.x & 63) == 0) {
+                __hip_atomic_store(state + 1, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(state + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky count
+            }
             break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -254,6 +267,26 @@ __device__ __forceinline__ void acquire_fence() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// One kernel build: WM waves of R output rows each (the 16-row tile), an NST-slot LDS ring (NST-1
+// K-chunks in flight).  <4, 4, 2>: two 4-wave workgroups per CU, one chunk in flight (the
+// round-3 first form); <8, 2, 4>: one 8-wave workgroup per CU, three chunks in flight, two tiles
+// of independent images interleaved per layer.
+template <int WM_, int R_, int NST_>
+struct TK {
+    static constexpr int WM = WM_, R = R_, NST = NST_;
+    static constexpr int NT = 64 * WM;
+    static_assert(R * WM == tk::TH, "16-row tiles");
+    static_assert(NST >= 2 && NST <= 4, "ring depth");
+    static constexpr int HPW = (tk::HP + WM - 1) / WM;   // halo pieces per wave (at most)
+    static constexpr int WPW = (tk::WPF + WM - 1) / WM;  // weight pieces per wave (at most)
+    static constexpr int SLOT = (tk::HP + tk::WPF) * 1024;
+    static constexpr int BIAS_OFF = NST * SLOT;          // 4 bias slots of 256 B
+    static constexpr int LDS = BIAS_OFF + 4 * 256;
+    static_assert(LDS <= 163840, "LDS budget");
+    static constexpr int BPC = 163840 / LDS < 2 ? 163840 / LDS : 2;  // workgroups per CU
+    static constexpr int WPS = BPC * WM / 4;                          // waves per SIMD
+};
+
 // Where the chunks of one (layer, tile) item come from (LDS-DMA through buffer resources:
 // 32-bit offsets, no per-piece 64-bit address arithmetic).
 struct Src {
@@ -264,16 +297,19 @@ struct Src {
     int wpc;         // weight pieces per chunk (9 / 18)
 };
 
+template <class K>
 struct TrunkCtx {
     unsigned* state;
     unsigned gen;
     int acquire;
     int hp, wp, cs16, pad, h, w, nbx, nby, ntiles;
     uint32_t pstride;            // bytes per 16-channel plane
-    uint32_t hoff[tk::HPW];      // per-lane halo piece offsets (chunk-invariant)
+    uint32_t hoff[K::HPW];       // per-lane halo piece offsets (chunk-invariant)
+    int abl;                     // tuning ablation bits (0 in production builds)
 };
 
-__device__ __forceinline__ Src src_of(const TrunkCtx& c, const_rec& rec, int t) {
+template <class C>
+__device__ __forceinline__ Src src_of(const C& c, const_rec& rec, int t) {
     const int bx = t % c.nbx, tmp = t / c.nbx, by = tmp % c.nby, img = tmp / c.nby;
     Src s;
     s.x = (const char*)(uintptr_t)rec.x;
@@ -304,31 +340,73 @@ __device__ __forceinline__ uint32_t halo_piece_off(int j, int lane, int wp) {
 
 // One chunk's LDS-DMA into ring slot `slot`: each wave its share of the 20 halo and 9 / 18
 // weight pieces; wave 0 also the bias (first chunk of a tile).  Halo pieces are sc1 (L1
-// bypass: other workgroups of this launch wrote them).
-__device__ __forceinline__ void stage_chunk(const TrunkCtx& c, const Src& s, int chunk, int slot, bool with_bias,
-                                            int bslot) {
+// bypass: other workgroups of this launch wrote them).  Returns the vector-memory instructions
+// this wave issued (wave-uniform), for the counted waits.
+template <int WM, int HPW, int WPW, int SLOTB, int BIASB>
+__device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t pstride, int abl, const Src& s,
+                                                  int chunk, int slot, bool with_bias, int bslot) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int wave = wave_id(), lane = threadIdx.x & 63;
-    char* dst = smem + slot * tk::SLOT;
+    char* dst = smem + slot * SLOTB;
+    uint32_t n = 0;
     const auto rx = rsrc(s.x);
-    const uint32_t so = s.h0 + (uint32_t)chunk * c.pstride;
-    if (!(trunk_abl() & 1))
+    const uint32_t so = s.h0 + (uint32_t)chunk * pstride;
+    if (!(abl & 1)) {
 #pragma unroll
-    for (int k = 0; k < tk::HPW; ++k)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, ISR_LDS_PTR(dst + (wave + tk::WM * k) * 1024), 16, c.hoff[k], so,
-                                                 0, 16);
+        for (int k = 0; k < HPW; ++k) {
+            const int j = wave + WM * k;
+            if (j < tk::HP) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, ISR_LDS_PTR(dst + j * 1024), 16, hoff[k], so, 0, 16);
+                ++n;
+            }
+        }
+    }
     const auto rw = rsrc(s.w);
     const uint32_t wo = (uint32_t)(chunk * s.wpc * 1024);
     char* wd = dst + tk::HP * 1024;
 #pragma unroll
-    for (int k = 0; k < (tk::WPF + tk::WM - 1) / tk::WM; ++k) {
-        const int j = wave + tk::WM * k;
-        if (j < s.wpc)
+    for (int k = 0; k < WPW; ++k) {
+        const int j = wave + WM * k;
+        if (j < s.wpc) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, ISR_LDS_PTR(wd + j * 1024), 16, lane * 16, wo + j * 1024, 0, 0);
+            ++n;
+        }
     }
-    if (with_bias && wave == 0 && lane < (s.wpc == tk::WPG ? 32 : 64))  // cout floats only
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(s.b), ISR_LDS_PTR(smem + tk::BIAS_OFF + bslot * 256), 4, lane * 4,
-                                                 0, 0, 0);
+    if (with_bias && wave == 0) {
+        if (lane < (s.wpc == tk::WPG ? 32 : 64))  // cout floats only
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(s.b), ISR_LDS_PTR(smem + BIASB + bslot * 256), 4,
+                                                     lane * 4, 0, 0, 0);
+        ++n;
+    }
+    return n;
+}
+
+template <class K>
+__device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src& s, int chunk, int slot, bool with_bias,
+                                                int bslot) {
+    return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF>(c.hoff, c.pstride, c.abl, s, chunk, slot,
+                                                                      with_bias, bslot);
+}
+
+// s_waitcnt vmcnt(n) for a run-time n (0..63): this wave's n youngest vector-memory
+// instructions may stay in flight.
+__device__ __forceinline__ void wait_vm(uint32_t n) {
+#define ISR_VMW(k)                                        \
+    case k:                                               \
+        asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); \
+        break;
+    switch (n) {
+        ISR_VMW(1) ISR_VMW(2) ISR_VMW(3) ISR_VMW(4) ISR_VMW(5) ISR_VMW(6) ISR_VMW(7) ISR_VMW(8) ISR_VMW(9)
+        ISR_VMW(10) ISR_VMW(11) ISR_VMW(12) ISR_VMW(13) ISR_VMW(14) ISR_VMW(15) ISR_VMW(16) ISR_VMW(17)
+        ISR_VMW(18) ISR_VMW(19) ISR_VMW(20) ISR_VMW(21) ISR_VMW(22) ISR_VMW(23) ISR_VMW(24) ISR_VMW(25)
+        ISR_VMW(26) ISR_VMW(27) ISR_VMW(28) ISR_VMW(29) ISR_VMW(30) ISR_VMW(31) ISR_VMW(32) ISR_VMW(33)
+        ISR_VMW(34) ISR_VMW(35) ISR_VMW(36) ISR_VMW(37) ISR_VMW(38) ISR_VMW(39) ISR_VMW(40) ISR_VMW(41)
+        ISR_VMW(42) ISR_VMW(43) ISR_VMW(44) ISR_VMW(45) ISR_VMW(46) ISR_VMW(47) ISR_VMW(48) ISR_VMW(49)
+        ISR_VMW(50) ISR_VMW(51) ISR_VMW(52) ISR_VMW(53) ISR_VMW(54) ISR_VMW(55) ISR_VMW(56) ISR_VMW(57)
+        ISR_VMW(58) ISR_VMW(59) ISR_VMW(60) ISR_VMW(61) ISR_VMW(62) ISR_VMW(63)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef ISR_VMW
 }
 
 // A operand of the residual fold: (1/s1) I on couts [16 h16, 16 h16 + 16) of a 32-cout
@@ -343,33 +421,70 @@ __device__ __forceinline__ bf16x8 fold_a_bits(uint32_t idv, int h16) {
     return __builtin_bit_cast(bf16x8, r);
 }
 
-// The item that follows the current tile in this workgroup's stream.
+// The tile that follows the current one in this workgroup's stream.
 struct Next {
     bool exists;
     int L, t;
     Src src;
-    int first_new;   // its first chunk its previous layer wrote (0: chunk 0 needs the wait)
+    int first_new;   // its first chunk its previous layer wrote (NEED_NONE on layer 0)
+    int nch;
     bool self_dep;   // its neighbourhood contains the tile being computed now
 };
 
-// Carried from item to item.
+// Per wave, carried from item to item (all wave-uniform).  Items are the K-chunks of the
+// stream in order; `issued` counts this wave's vector-memory instructions, and m[0..] holds
+// `issued` right after the DMA of the current item and of the items staged after it, so the
+// top of an item waits for exactly its own DMA (wait_vm(issued - m[0])) and leaves the later
+// items, stores and loads in flight.
+template <class K>
 struct Stream {
-    int item;        // chunk counter (ring slot = item & 1)
-    int tseq;        // tile counter (bias slot = tseq & 1)
-    bool staged;     // this wave issued the DMA of the next chunk
-    bool mixed;      // that decision came from a per-wave poll (waves may disagree)
-    int pend_t;      // tile whose progress word is still to be published (-1: none)
+    int item;             // global index of the item being computed
+    int staged;           // global index of the last item whose DMA was issued
+    int tseq;             // tiles started (bias slot = tseq & 3)
+    uint32_t issued;
+    uint32_t m0, m1, m2, m3;  // FIFO: m0 = current item (named scalars: an array would be indexed
+                              // at run time and live in scratch, whose ops count in vmcnt)
+    int pend_t;           // tile whose progress word waits for its stores (-1: none)
     unsigned pend_v;
-    unsigned pollv;  // early poll of the next dependency (issued one chunk ahead)
-    bool polled;
-    bool dep_next;   // this wave verified the next tile's neighbourhood when staging its chunk 0
+    uint32_t pend_mark;   // `issued` right after those stores
+    bool dep_next;        // the next tile's neighbourhood has been verified
 };
 
-template <int NF>
-__device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_rec& rec, int L, int t,
+template <class K>
+__device__ __forceinline__ void push_mark(Stream<K>& st) {
+    const int pos = st.staged - st.item;  // position of the item just staged
+    const uint32_t v = st.issued;
+    st.m0 = pos == 0 ? v : st.m0;
+    st.m1 = pos == 1 ? v : st.m1;
+    st.m2 = pos == 2 ? v : st.m2;
+    st.m3 = pos >= 3 ? v : st.m3;
+}
+
+template <class K>
+__device__ __forceinline__ void pop_mark(Stream<K>& st) {
+    st.m0 = st.m1;
+    st.m1 = st.m2;
+    st.m2 = st.m3;
+}
+
+// Publish the pending tile's progress word now (every wave drains all its vector memory, then a
+// workgroup barrier): required before any blocking wait, so that no workgroup ever spins on a
+// word this workgroup holds back.  Wave-uniform call sites only (it contains a barrier).
+template <class K>
+__device__ __forceinline__ void force_publish(const TrunkCtx<K>& c, Stream<K>& st) {
+    if (st.pend_t < 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(c.state + 4 + st.pend_t, st.pend_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st.pend_t = -1;
+}
+
+template <class K, int NF>
+__device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, const_rec& rec, int L, int t,
                                          const Next& nx) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int R = tk::R, CT = 32 * NF, TN = 3, NA = R + 2;
+    constexpr int R = K::R, NST = K::NST, CT = 32 * NF, TN = 3, NA = R + 2;
     const int wave = wave_id(), lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
     const int bx = t % c.nbx, tmp = t / c.nbx, by = tmp % c.nby, img = tmp / c.nby;
     const int x0 = bx * tk::TW, y0 = by * tk::TH;
@@ -377,10 +492,12 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
     const int first_new = rec_first_new(rec);  // NEED_NONE on layer 0
     const unsigned need = c.gen * 1024u + (unsigned)L;  // the neighbourhood is done with layer L-1
     const bool fold = NF == 2 && rec_fold(rec);
+    const bool has_r2 = NF == 2 && rec.r2 != 0;
     const Src me = src_of(c, rec, t);
-    bool dep_ok = first_new == tk::NEED_NONE || (first_new == 0 && st.dep_next);
+    bool dep_ok = first_new == tk::NEED_NONE || st.dep_next;
     st.dep_next = false;
-    const int bslot = st.tseq & 1;
+    const int bslot = st.tseq & 3;
+    const int first_item = st.item;  // this tile's chunk 0
     trunk_stamp(L, t, c.ntiles, 0);
 
     // per-lane LDS read addresses (slot 0): weights A[n][k] (n = cout), halo rows of this wave
@@ -390,44 +507,48 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
     for (int dx = 0; dx < 3; ++dx)
         a_h[dx] = (uint32_t)((wave * R * tk::HC + l31 + dx) * 32 + 16 * (hh ^ (((l31 + dx) >> 3) & 1)));
 
+    // neighbourhood wait (blocking), preceded by the pending publish
+    auto wait_deps = [&](int tt, unsigned nd) {
+        force_publish(c, st);
+        trunk_stamp(L, t, c.ntiles, 4);
+        dep_wait(c.state, nb_of(tt, c.nbx, c.nby), nd, c.gen);
+        if (c.acquire) acquire_fence();
+        trunk_stamp(L, t, c.ntiles, 5);
+    };
+
     f32x16 acc[R][NF];
+    bf16x8 q2[R][NF][2];
+    uint32_t r2_mark = 0;
 
     for (int ch = 0; ch < nch; ++ch, ++st.item) {
-        const int slot = st.item & 1;
-        // ---- top of item: the chunk has landed for every wave; publish the previous tile ----
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (st.mixed) *reinterpret_cast<volatile int*>(smem + tk::FLAG_OFF + 4 * wave) = st.staged ? 0 : 1;
+        const int slot = st.item % NST;
+        const bool stamp_tile = t == (int)blockIdx.x;
+        item_stamp(L, stamp_tile, ch, 0, K::WM);
+        // ---- top of item: this item's DMA has landed for every wave ----
+        if (st.staged < st.item) {
+            // not staged (the next tile needed this tile's own outputs): drain, publish, wait, stage
+            force_publish(c, st);
+            if (ch >= first_new && !dep_ok) {
+                wait_deps(t, need);
+                dep_ok = true;
+            }
+            st.issued += stage_chunk(c, me, ch, slot, ch == 0, bslot);
+            st.staged = st.item;
+            push_mark(st);
+        }
+        wait_vm(st.issued - st.m0);
+        item_stamp(L, stamp_tile, ch, 1, K::WM);
         raw_barrier();
-        if (st.pend_t >= 0) {
+        item_stamp(L, stamp_tile, ch, 2, K::WM);
+        if (st.pend_t >= 0 && (int)(st.m0 - st.pend_mark) >= 0) {  // its stores are older than this DMA
             if (threadIdx.x == 0)
                 __hip_atomic_store(c.state + 4 + st.pend_t, st.pend_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             st.pend_t = -1;
         }
-        bool any_deferred = !st.staged;
-        if (st.mixed) {
-            const volatile int* fl = reinterpret_cast<const volatile int*>(smem + tk::FLAG_OFF);
-            any_deferred = (fl[0] | fl[1] | fl[2] | fl[3]) != 0;
-        }
-        if (any_deferred) {  // uniform: a deferred refill — wait for the neighbourhood, stage, land
-            if (!st.staged) {
-                if (ch >= first_new && !dep_ok) {
-                    trunk_stamp(L, t, c.ntiles, 4);
-                    dep_wait(c.state, nb_of(t, c.nbx, c.nby), need, c.gen);
-                    if (c.acquire) acquire_fence();
-                    trunk_stamp(L, t, c.ntiles, 5);
-                }
-                stage_chunk(c, me, ch, slot, ch == 0, bslot);
-            }
-            if (ch >= first_new) dep_ok = true;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            raw_barrier();
-        }
-        st.staged = true;
-        st.mixed = false;
         if (ch == 0) {
             trunk_stamp(L, t, c.ntiles, 1);
             // bias → accumulators (register g of lane l: cout (g&3) + 8(g>>2) + 4hh of fragment f)
-            const float* bs = reinterpret_cast<const float*>(smem + tk::BIAS_OFF + bslot * 256);
+            const float* bs = reinterpret_cast<const float*>(smem + K::BIAS_OFF + bslot * 256);
 #pragma unroll
             for (int f = 0; f < NF; ++f) {
                 f32x16 b0;
@@ -441,26 +562,33 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
                 for (int r = 0; r < R; ++r) acc[r][f] = b0;
             }
         }
-        // ---- the chunk after this one: may its DMA be issued now? ----
-        const bool last = ch + 1 == nch;
-        bool issue_next = false, checks = false, nx_checks = false;
-        if (!last) {
-            issue_next = true;
-            checks = ch + 1 >= first_new && !dep_ok;
-        } else if (nx.exists) {
-            // the next item's chunk 0 needs the wait when its previous layer wrote it; when the
-            // tile computed now is in its neighbourhood, it cannot be staged before this tile's
-            // stores land (deferred to the top of the next item)
-            const bool needs = nx.first_new == 0 && nx.L > 0;
-            issue_next = !(needs && nx.self_dep);
-            checks = nx_checks = issue_next && needs;
+        if (has_r2 && ch + 1 == nch) {
+            // RRDB residual of the epilogue, loaded now (older than the refill DMA below).  Ordinary
+            // (compiler-visible) loads: an asm load's destination may be copied or spilled by the
+            // register allocator before the data arrives; hipcc's own wait before their first use
+            // is at worst a full vmcnt(0), once per RRDB
+            const int xx = x0 + l31;
+            const uint32_t plane_px = (uint32_t)(c.hp * c.wp);
+            const uint32_t r2pl = (uint32_t)(img * c.cs16 + rec_r2p(rec)) * plane_px;
+            const auto rr = rsrc((const char*)(uintptr_t)rec.r2);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t pix = (uint32_t)((y0 + wave * R + r + c.pad) * c.wp + xx + c.pad);
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int blk = 0; blk < 2; ++blk) {
+                        const int co = f * 32 + 16 * blk + 8 * hh;
+                        q2[r][f][blk] = __builtin_bit_cast(
+                            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                        rr, (r2pl + (uint32_t)(co >> 4) * plane_px + pix) * 32 + 16 * hh, 0, 16));
+                    }
+            }
+            st.issued += R * NF * 2;
+            r2_mark = st.issued;
         }
-        // early poll for the NEXT item's refill (its answer lands by that item's top-of-item
-        // vmcnt): the dependency of own chunk ch + 2, or of the next tile's chunk 0
-        const bool poll_own = ch + 2 < nch && ch + 2 == first_new && !dep_ok;
-        const bool poll_nx = ch + 2 == nch && nx.exists && nx.first_new == 0 && nx.L > 0 && !nx.self_dep;
 
-        const char* sb = smem + slot * tk::SLOT;
+        const char* sb = smem + slot * K::SLOT;
         bf16x8 fb[2][TN][NF], fa[2][NA];
         auto read_one = [&](int dx, int idx, int set) {
             if (idx < TN * NF) {
@@ -471,11 +599,11 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
                 fa[set][ia] = lds_read16(sb + a_h[dx] + ia * tk::HC * 32);
             }
         };
-        // step 0's fragments in order of first use (dy-major MFMA order below)
         auto read_fb = [&](int dx, int dyi, int set) {
 #pragma unroll
             for (int f = 0; f < NF; ++f) read_one(dx, dyi * NF + f, set);
         };
+        // step 0's fragments in order of first use (kernel-row-major MFMA order below)
         read_fb(0, 0, 0);
 #pragma unroll
         for (int ia = 0; ia < R; ++ia) read_one(0, TN * NF + ia, 0);
@@ -484,41 +612,38 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
         read_fb(0, 2, 0);
         read_one(0, TN * NF + R + 1, 0);
         __builtin_amdgcn_sched_barrier(0);
-        // ---- refill: the next chunk (own, or the next item's first) into the other slot ----
-        if (issue_next) {
-            bool go = true;
-            if (checks) {
-                const int nbq = nx_checks ? nb_of(nx.t, c.nbx, c.nby) : nb_of(t, c.nbx, c.nby);
-                const unsigned needq = nx_checks ? c.gen * 1024u + (unsigned)nx.L : need;
-                const unsigned v = st.polled ? st.pollv : poll_load(c.state + 4, nbq);
-                go = __all(nbq < 0 || (int)(v - needq) >= 0);
-                if (go && c.acquire) acquire_fence();
+
+        // ---- refill: stage the stream up to NST-1 items ahead (own chunks, then the next tile's) ----
+        while (st.staged < st.item + NST - 1) {
+            const int off = st.staged + 1 - first_item;  // chunk offset from this tile's chunk 0
+            const int nslot = (st.staged + 1) % NST;
+            if (off < nch) {
+                if (off >= first_new && !dep_ok) {
+                    wait_deps(t, need);
+                    dep_ok = true;
+                }
+                st.issued += stage_chunk(c, me, off, nslot, false, 0);
+            } else {
+                const int nc = off - nch;
+                if (!nx.exists || nc >= nx.nch) break;
+                if (nx.L > 0 && nc >= nx.first_new && !st.dep_next) {
+                    if (nx.self_dep) break;  // needs this tile's outputs: staged at its own top
+                    wait_deps(nx.t, c.gen * 1024u + (unsigned)nx.L);
+                    st.dep_next = true;
+                }
+                st.issued += stage_chunk(c, nx.src, nc, nslot, nc == 0, (bslot + 1) & 3);
             }
-            if (go) {
-                if (!last) stage_chunk(c, me, ch + 1, slot ^ 1, false, 0);
-                else stage_chunk(c, nx.src, 0, slot ^ 1, true, bslot ^ 1);
-                if (checks && !last) dep_ok = true;
-                if (checks && last) st.dep_next = true;
-            }
-            st.staged = go;
-            st.mixed = checks;
-        } else {
-            st.staged = !(last && nx.exists);  // nothing follows: nothing to stage
-            st.mixed = false;
-        }
-        st.polled = false;
-        if (poll_own || poll_nx) {
-            const int nbq = poll_nx ? nb_of(nx.t, c.nbx, c.nby) : nb_of(t, c.nbx, c.nby);
-            st.pollv = poll_load(c.state + 4, nbq);
-            st.polled = true;
+            ++st.staged;
+            push_mark(st);
         }
         __builtin_amdgcn_sched_barrier(0);
+        item_stamp(L, stamp_tile, ch, 3, K::WM);
+
         // ---- MFMAs: 3 steps (dx), each in kernel-row-major order (dy, then output row r):
         // every accumulator still sees dy 0, 1, 2 in that order (conv3x3.hip's input-row-major
         // loop gives each accumulator the same sequence, so the bits agree).  The next step's
         // fragment of kernel row dy is read right after that row's last MFMA here, and its
-        // input row ia right after the current one's last use — one live register set plus
-        // the rows in flight, each read ~16 MFMAs before it is needed. ----
+        // input row ia right after the current one's last use. ----
 #pragma unroll
         for (int stp = 0; stp < 3; ++stp) {
             const int cur = stp & 1;
@@ -527,10 +652,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
 #pragma unroll
-                    for (int f = 0; f < NF; ++f) {
-                        if (trunk_abl() & 2) asm volatile("" ::"v"(fb[cur][dyi][f]), "v"(fa[cur][r + dyi]));
-                        else acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][r + dyi], acc[r][f]);
-                    }
+                    for (int f = 0; f < NF; ++f) acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][r + dyi], acc[r][f]);
                     if constexpr (NF == 2) {
                         // residual fold: + x/s1 on the centre pixels of row r (dx = 1, dy = 1),
                         // between the row's dy = 1 and dy = 2 contributions
@@ -550,41 +672,25 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
                 }
             }
         }
+        item_stamp(L, stamp_tile, ch, 4, K::WM);
+        pop_mark(st);  // the FIFO head moves to the next item (marks are positions from st.item)
     }
     trunk_stamp(L, t, c.ntiles, 2);
 
     // the neighbourhood must be done with layer L-1 before this tile's outputs land (a layer
     // that reads nothing its predecessor wrote never waited above)
-    if (!dep_ok && first_new != tk::NEED_NONE) dep_wait(c.state, nb_of(t, c.nbx, c.nby), need, c.gen);
+    if (!dep_ok && first_new != tk::NEED_NONE) wait_deps(t, need);
 
     // ---- epilogue: straight from the accumulators, write-through (sc1) stores ----
     {
         typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
         const int xx = x0 + l31;
         const auto yr = __builtin_amdgcn_make_buffer_rsrc((char*)(uintptr_t)rec.y, (short)0, 0x7fffffff, 0x00020000);
-        const bool has_r2 = NF == 2 && rec.r2 != 0;
-        const auto rr = __builtin_amdgcn_make_buffer_rsrc((char*)(uintptr_t)rec.r2, (short)0, 0x7fffffff, 0x00020000);
         const float slope = rec.slope, s1 = rec.s1, s2 = rec.s2;
         const bool scale2 = s2 != 1.f;
         const uint32_t plane_px = (uint32_t)(c.hp * c.wp);
-        // channel-plane offsets (in pixels) of this lane's first y / r2 plane
         const uint32_t ypl = (uint32_t)(img * c.cs16 + rec_yp(rec)) * plane_px;
-        const uint32_t r2pl = (uint32_t)(img * c.cs16 + rec_r2p(rec)) * plane_px;
-        bf16x8 q2[R][NF][2];
-        if (has_r2) {  // RRDB residual: every load of the tile issued before any use
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint32_t pix = (uint32_t)((y0 + wave * R + r + c.pad) * c.wp + xx + c.pad);
-#pragma unroll
-                for (int f = 0; f < NF; ++f)
-#pragma unroll
-                    for (int blk = 0; blk < 2; ++blk) {
-                        const int co = f * 32 + 16 * blk + 8 * hh;
-                        const uint32_t off = (r2pl + (uint32_t)(co >> 4) * plane_px + pix) * 32 + 16 * hh;
-                        q2[r][f][blk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 16));
-                    }
-            }
-        }
+        if (has_r2) wait_vm(st.issued - r2_mark);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int yy = y0 + wave * R + r;
@@ -619,8 +725,10 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
                     bf16x8 tq;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) tq[e] = (__bf16)u[e];
-                    if (!(trunk_abl() & 4))
+                    if (!(c.abl & 4)) {
                         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tq), yr, off, 0, 16);
+                        ++st.issued;
+                    }
                 }
             }
         }
@@ -628,18 +736,23 @@ __device__ __forceinline__ void run_tile(const TrunkCtx& c, Stream& st, const_re
     trunk_stamp(L, t, c.ntiles, 3);
     st.pend_t = t;
     st.pend_v = c.gen * 1024u + (unsigned)(L + 1);
+    st.pend_mark = st.issued;
     ++st.tseq;
 }
 
-__global__ __launch_bounds__(tk::NT, 2) void trunk_kernel(TrunkArgs a) {
-    TrunkCtx c;
+template <class K>
+__global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
+    TrunkCtx<K> c;
     c.state = a.state;
     c.acquire = a.acquire;
     c.gen = __hip_atomic_load(a.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const_geo& g = *(const_geo*)(uintptr_t)(a.state + a.rec_off - 16);
     const_rec* recs = (const_rec*)(uintptr_t)(a.state + a.rec_off);
     if (g.err != 0) {  // the prep kernel refused the layer table: give up loudly
-        if (threadIdx.x == 0) __hip_atomic_store(a.state + 1, c.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(a.state + 1, c.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.state + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         return;
     }
     c.hp = g.hp;
@@ -652,24 +765,26 @@ __global__ __launch_bounds__(tk::NT, 2) void trunk_kernel(TrunkArgs a) {
     c.nby = g.nby;
     c.ntiles = g.ntiles;
     c.pstride = (uint32_t)(c.hp * c.wp * 32);
+    c.abl = trunk_abl_load();
     {
         const int wave = wave_id(), lane = threadIdx.x & 63;
 #pragma unroll
-        for (int k = 0; k < tk::HPW; ++k) c.hoff[k] = halo_piece_off(wave + tk::WM * k, lane, c.wp);
+        for (int k = 0; k < K::HPW; ++k) c.hoff[k] = halo_piece_off(wave + K::WM * k, lane, c.wp);
     }
     const int G = gridDim.x, b = blockIdx.x;
-    Stream st;
+    Stream<K> st;
     st.item = 0;
+    st.staged = 0;
     st.tseq = 0;
+    st.issued = 0;
+    st.m0 = st.m1 = st.m2 = st.m3 = 0;
     st.pend_t = -1;
     st.pend_v = 0;
-    st.mixed = false;
-    st.polled = false;
-    st.pollv = 0;
+    st.pend_mark = 0;
     st.dep_next = false;
-    st.staged = true;
     if (b < c.ntiles) {
-        stage_chunk(c, src_of(c, recs[0], b), 0, 0, true, 0);  // layer 0 reads the trunk input only
+        st.issued += stage_chunk(c, src_of(c, recs[0], b), 0, 0, true, 0);  // layer 0 reads the trunk input only
+        st.m0 = st.issued;
         for (int L = 0; L < a.nl; ++L) {
             const_rec& rec = recs[L];
             for (int t = b; t < c.ntiles; t += G) {
@@ -689,13 +804,14 @@ __global__ __launch_bounds__(tk::NT, 2) void trunk_kernel(TrunkArgs a) {
                 const_rec& nrec = recs[nx.L];
                 nx.src = src_of(c, nrec, nx.t);
                 nx.first_new = rec_first_new(nrec);
+                nx.nch = rec_nch(nrec);
                 {
                     const int bx = t % c.nbx, tq = t / c.nbx, by = tq % c.nby, im = tq / c.nby;
                     const int bx2 = nx.t % c.nbx, nq = nx.t / c.nbx, by2 = nq % c.nby, im2 = nq / c.nby;
                     nx.self_dep = im == im2 && abs(bx - bx2) <= 1 && abs(by - by2) <= 1;
                 }
-                if (rec_kind(rec) == 0) run_tile<1>(c, st, rec, L, t, nx);
-                else run_tile<2>(c, st, rec, L, t, nx);
+                if (rec_kind(rec) == 0) run_tile<K, 1>(c, st, rec, L, t, nx);
+                else run_tile<K, 2>(c, st, rec, L, t, nx);
             }
         }
     }
@@ -707,8 +823,9 @@ __global__ __launch_bounds__(tk::NT, 2) void trunk_kernel(TrunkArgs a) {
 
 // Grid: every workgroup must be resident at once (tiles wait on other workgroups' tiles), so
 // the grid is min(tiles, resident workgroups) with residency from the occupancy API (capped at
-// the 2 per CU the kernel is built for); ISR_ERR when that is below one workgroup per CU.
-int trunk_launch(const isr_chain_desc* cd, hipStream_t s) {
+// what the build is made for); ISR_ERR when that is below one workgroup per CU.
+template <class K>
+static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
     if (cd->ha % tk::TH || cd->wa % tk::TW || cd->nl < 1 || cd->nl > 1024) return -2;
     const int nbx = cd->wa / tk::TW, nby = cd->ha / tk::TH;
     const long long ntiles = (long long)cd->n * nbx * nby;
@@ -716,23 +833,23 @@ int trunk_launch(const isr_chain_desc* cd, hipStream_t s) {
     static thread_local int cached_dev = -1, cached_per_cu = 0, cached_cus = 0;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
+    const void* kern = (const void*)trunk_kernel<K>;
     if (dev != cached_dev) {
-        (void)hipFuncSetAttribute((const void*)trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, tk::LDS);
+        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trunk_kernel, tk::NT, tk::LDS) !=
-            hipSuccess)
-            return -1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, K::NT, K::LDS) != hipSuccess) return -1;
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return -1;
         cached_dev = dev;
-        cached_per_cu = per_cu < 2 ? per_cu : 2;
+        cached_per_cu = per_cu < K::BPC ? per_cu : K::BPC;
         cached_cus = cus;
     }
+    int per_cu = cached_per_cu;
 #ifdef ISR_TUNING
-    if (g_trunk_per_cu > 0 && g_trunk_per_cu < cached_per_cu) cached_per_cu = g_trunk_per_cu;
+    if (g_trunk_per_cu > 0 && g_trunk_per_cu < per_cu) per_cu = g_trunk_per_cu;
 #endif
-    if (cached_per_cu < 1) return -4;
-    const long long slots = (long long)cached_per_cu * cached_cus;
+    if (per_cu < 1) return -4;
+    const long long slots = (long long)per_cu * cached_cus;
     const int grid = (int)(ntiles < slots ? ntiles : slots);
     const int rec_off = (int)trunk_rec_off((int)ntiles);
     hipLaunchKernelGGL(trunk_prep_kernel, dim3(1), dim3(1024), 16, s, cd->layers, cd->kinds, cd->nl, cd->n, cd->ha,
@@ -742,8 +859,15 @@ int trunk_launch(const isr_chain_desc* cd, hipStream_t s) {
     a.rec_off = rec_off;
     a.nl = cd->nl;
     a.acquire = cd->acquire;
-    hipLaunchKernelGGL(trunk_kernel, dim3(grid), dim3(tk::NT), tk::LDS, s, a);
+    hipLaunchKernelGGL(trunk_kernel<K>, dim3(grid), dim3(K::NT), K::LDS, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+using TK_DEEP = TK<8, 2, 4>;   // production: one 8-wave workgroup per CU, 3 chunks in flight
+using TK_PAIR = TK<4, 4, 2>;   // two 4-wave workgroups per CU, 1 chunk in flight
+
+int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
+    return form == 1 ? trunk_launch_k<TK_PAIR>(cd, s) : trunk_launch_k<TK_DEEP>(cd, s);
 }
 
 #ifdef ISR_TUNING
@@ -752,9 +876,13 @@ int trunk_knobs_set(const int* k) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
 }
 int trunk_stamps_set(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+int trunk_item_stamps_set(void* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_item_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
 #else
 int trunk_knobs_set(const int*) { return -2; }
 int trunk_stamps_set(void*) { return -2; }
+int trunk_item_stamps_set(void*) { return -2; }
 #endif
 
 }  // namespace isr

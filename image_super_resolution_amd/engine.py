@@ -234,6 +234,16 @@ class GeneratorPlan:
             self.chain.poll()
         return out
 
+    @property
+    def chains(self) -> list:
+        return [self.chain] if self.chain is not None else []
+
+    def verify(self) -> None:
+        """Blocking give-up check of every forward queued so far (one-shot consumers call it
+        before handing results out: the tiler's canvas, a training epoch end)."""
+        for c in self.chains:
+            c.verify()
+
 
 class ChainFailed(RuntimeError):
     """A persistent-chain dependency wait gave up (a neighbour tile never published: the
@@ -288,28 +298,51 @@ class ConvChain:
             self.fn = lambda d, s: fv(d, var, s)
 
     def failed(self) -> bool:
-        """True when a dependency wait gave up in the last launch (results invalid)."""
+        """True when a dependency wait gave up in the last launch (results invalid).  Synchronous
+        (tests and tools)."""
         gen, fail = self.state[:2].tolist()
         return gen != 0 and fail == gen
 
+    # ---- product-path checks.  state[2] counts give-ups over every launch and is never reset,
+    # so a snapshot taken after ANY later launch still shows an earlier failure (the video
+    # pipeline's double-buffered slots can read a newer snapshot than the batch they check).
+    def snapshot(self, dst: torch.Tensor) -> None:
+        """Enqueue (current stream) an async copy of the give-up count into pinned `dst` (int32[1])."""
+        dst.copy_(self.state[2:3], non_blocking=True)
+
+    def check_count(self, count: int) -> None:
+        """Raise ChainFailed when `count` (a snapshot) shows a give-up not yet reported."""
+        seen = getattr(self, "_fails_seen", 0)
+        if count != seen:
+            self._fails_seen = count
+            raise ChainFailed("conv chain: a dependency wait gave up (launch not fully resident); "
+                              "outputs of that forward are invalid")
+
     def poll(self) -> None:
-        """Lagged, non-blocking failure check for the product path: raises ChainFailed when an
-        earlier launch's (generation, give-up) words — copied asynchronously to pinned memory
-        after it — show a wait that gave up; then queues the copy for the launch just issued.
-        Never synchronises (an unfinished copy is checked on a later call)."""
+        """Lagged, non-blocking check after every eager forward: raises ChainFailed when the
+        snapshot queued after an earlier launch shows a give-up; then queues a snapshot after the
+        launch just issued.  Never synchronises (an unfinished copy is checked on a later call)."""
         ev = getattr(self, "_poll_ev", None)
         if ev is not None and ev.query():
-            gen, fail = self._poll_host.tolist()
-            if gen != 0 and fail == gen:
-                raise ChainFailed("conv chain: a dependency wait gave up (launch not fully resident); "
-                                  "outputs of that forward are invalid")
+            self.check_count(int(self._poll_host[0]))
         elif ev is not None:
             return  # the previous copy has not landed yet: keep it, check it later
         if getattr(self, "_poll_host", None) is None:
-            self._poll_host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+            self._poll_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._poll_ev = torch.cuda.Event()
-        self._poll_host.copy_(self.state[:2], non_blocking=True)
+        self.snapshot(self._poll_host)
         self._poll_ev.record()
+
+    def verify(self) -> None:
+        """Blocking check of every launch queued so far on the current stream (waits for them,
+        not for the whole device): raises ChainFailed on a give-up."""
+        if getattr(self, "_verify_host", None) is None:
+            self._verify_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._verify_ev = torch.cuda.Event()
+        self.snapshot(self._verify_host)
+        self._verify_ev.record()
+        self._verify_ev.synchronize()
+        self.check_count(int(self._verify_host[0]))
 
 
 class SplitGeneratorPlan:
@@ -326,8 +359,11 @@ class SplitGeneratorPlan:
             raise ValueError(f"batch {n} does not split into {splits} equal sub-batches")
         self.m = n // splits
         self.key = (n, h, w, str(device), x_u8, out_u8, tuple(mean), tuple(std), splits, stagger_us)
+        # no persistent chain in the sub-plans: their launches run concurrently on separate
+        # streams, and two grids that each fill the device cannot all be resident (waits would
+        # give up); the split plan is the per-conv form only
         self.subs = [GeneratorPlan(gw, self.m, h, w, device, x_u8, out_u8, mean, std, variants=variants,
-                                   chain=chain) for _ in range(splits)]
+                                   chain=False) for _ in range(splits)]
         self.out_shape = (n,) + self.subs[0].out_shape[1:]
         self.out_dtype = self.subs[0].out_dtype
         self.streams = [torch.cuda.Stream(device) for _ in range(splits)]
@@ -358,6 +394,11 @@ class SplitGeneratorPlan:
         for s in self.streams:
             cur.wait_stream(s)
         return out
+
+    chains: list = []
+
+    def verify(self) -> None:
+        pass
 
 
 _SLEEP_CAL: list[float] = []
@@ -422,7 +463,12 @@ class GraphedPlan:
 
     def run(self) -> torch.Tensor:
         self.graph.replay()
+        for c in self.plan.chains:  # outside the graph: a lagged, non-blocking give-up check
+            c.poll()
         return self.out
+
+    def verify(self) -> None:
+        self.plan.verify()
 
 
 def make_plan(gw: GeneratorWeights, n: int, h: int, w: int, device, x_u8: bool, out_u8: bool, mean, std,

@@ -361,11 +361,12 @@ def fuse_conv_and_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
     fused = nn.Conv2d(conv.in_channels, conv.out_channels, kernel_size=conv.kernel_size, stride=conv.stride,
                       padding=conv.padding, groups=conv.groups, bias=True).to(conv.weight.device)
     fused.requires_grad_(False)
-    s = bn.weight.div(torch.sqrt(bn.eps + bn.running_var))
-    fused.weight.copy_(conv.weight * s.view(-1, 1, 1, 1))
-    b_conv = torch.zeros(conv.weight.size(0), device=conv.weight.device) if conv.bias is None else conv.bias
-    b_bn = bn.bias - bn.weight.mul(bn.running_mean).div(torch.sqrt(bn.running_var + bn.eps))
-    fused.bias.copy_(s * b_conv + b_bn)
+    with torch.no_grad():  # the fused weights are leaves with no autograd history
+        s = bn.weight.div(torch.sqrt(bn.eps + bn.running_var))
+        fused.weight.copy_(conv.weight * s.view(-1, 1, 1, 1))
+        b_conv = torch.zeros(conv.weight.size(0), device=conv.weight.device) if conv.bias is None else conv.bias
+        b_bn = bn.bias - bn.weight.mul(bn.running_mean).div(torch.sqrt(bn.running_var + bn.eps))
+        fused.bias.copy_(s * b_conv + b_bn)
     return fused
 
 

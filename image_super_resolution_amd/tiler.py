@@ -136,6 +136,11 @@ class GeneratorRunner:
         out = torch.empty(plan.out_shape, dtype=torch.uint8, device=self.device)
         return plan.run(x.contiguous(), out)
 
+    def verify(self) -> None:
+        """Blocking persistent-chain give-up check of every forward issued so far (engine.ChainFailed)."""
+        for plan in self.plans.values():
+            plan.verify()
+
     def free(self):
         self.plans.clear()
 
@@ -208,6 +213,9 @@ class TileUpscaler:
         tiles = plan_tiles(H, W, self.window, self.halo)
         mine = shard_tiles(tiles, world)[rank] if world > 1 else tiles
         done = self.run_tiles(image, mine)
+        verify = getattr(self.runner, "verify", None)
+        if verify is not None:
+            verify()  # every forward of this image, the last included, before anything is stitched
         if world == 1:
             canvas = torch.zeros((c, H * s, W * s), dtype=torch.uint8, device=self.device)
             for t in tiles:

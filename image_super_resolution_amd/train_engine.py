@@ -34,6 +34,7 @@ import ctypes
 from dataclasses import dataclass
 
 import torch
+import torch.distributed as dist
 from torch import nn
 
 from . import ops
@@ -256,7 +257,7 @@ class GeneratorTrainPlan:
             extra = dict(r2=D[j - 2], s2=a) if j % 3 == 2 else {}
             conv_bn(D[j], 192, c, D[j + 1], 0, Zj, 0, 1.0, r1=D[j], s1=a, **extra)
         self.chain = None
-        if not self.has_bn and self.rdbs and _os.environ.get("ISR_TRAIN_CHAIN", "1") == "1":
+        if not self.has_bn and self.rdbs and _os.environ.get("ISR_TRAIN_CHAIN", "1") == "1" and not _device_shared():
             # no BatchNorm: the whole trunk forward as ONE persistent isr_conv_chain launch (as
             # inference, engine.ConvChain); every RDB writes its own dense buffer here
             from .engine import ConvChain
@@ -540,6 +541,25 @@ class _GeneratorFn(torch.autograd.Function):
     def backward(ctx, gy):
         grads = ctx.plan.backward(gy.contiguous().float())
         return (None, None, *grads)
+
+
+def _device_shared() -> bool:
+    """True when several ranks of this job drive one GPU (gloo over CUDA tensors, or more local
+    ranks than devices): two persistent-chain grids on one device cannot both be resident, so
+    the training plan runs its trunk per conv then."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    local = int(_os.environ.get("LOCAL_WORLD_SIZE", dist.get_world_size()))
+    return dist.get_backend() == "gloo" or local > max(1, torch.cuda.device_count())
+
+
+def verify_chains(gen: nn.Module) -> None:
+    """Blocking persistent-chain give-up check of every training forward queued so far on this
+    generator (engine.ChainFailed); the trainer calls it at the end of every epoch, before the
+    epoch's results (losses, checkpoint) are handed out."""
+    plan = gen.__dict__.get("_isr_train_plan")
+    if plan is not None and plan.chain is not None:
+        plan.chain.verify()
 
 
 def get_train_plan(gen: nn.Module, x: torch.Tensor) -> GeneratorTrainPlan:

@@ -84,7 +84,15 @@ def train(model, ema: ModelEMA, batches, transform, compute_loss, optimizer, gra
                 _scalar(tensorBoard, "loss", v, epoch * total + idx - len(vals) + k + 2)
             losses += vals
             pending = []
+    _verify(model)
     return losses
+
+
+def _verify(gen) -> None:
+    """Epoch end: a persistent-chain give-up anywhere in the epoch raises here (engine.ChainFailed),
+    before the caller logs the epoch or saves its checkpoint."""
+    from .train_engine import verify_chains
+    verify_chains(_unwrap(gen))
 
 
 def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_loss, optimizer_g, optimizer_d,
@@ -147,6 +155,7 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
                 _scalar(tensorBoard, "loss/dis", d, step)
                 loss_g.append(c)
             pending = []
+    _verify(gen_net)
     return loss_g
 
 

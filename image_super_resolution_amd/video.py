@@ -328,6 +328,8 @@ class FrameUpscaler:
                 self.x_hwc[b:].zero_()
         self.run_async()
         self.stream.synchronize()
+        with torch.cuda.stream(self.stream):
+            self.plan.verify()  # a persistent-chain give-up raises before the frames are handed out
         return self.bgr[:b]
 
 
@@ -345,6 +347,10 @@ class VideoUpscaler:
         self.pin_out = [torch.empty((b, H, W, 3), dtype=torch.uint8).pin_memory() for _ in range(2)]
         self.h2d_done = [torch.cuda.Event(), torch.cuda.Event()]
         self.d2h_done = [torch.cuda.Event(), torch.cuda.Event()]
+        # per output slot: the chains' give-up counts, copied right after that batch's forward
+        # (outside the captured graph) and checked by the writer before the batch is encoded
+        self.chains = list(up.plan.chains)
+        self.pin_state = [torch.zeros(max(1, len(self.chains)), dtype=torch.int32).pin_memory() for _ in range(2)]
 
     def run(self, frames, recorder, max_frames: int | None = None) -> int:
         """Upscale every frame of `frames` (iterable of uint8 HWC RGB arrays) into
@@ -365,6 +371,8 @@ class VideoUpscaler:
                 try:
                     if not err:
                         self.d2h_done[slot].synchronize()
+                        for k, c in enumerate(self.chains):  # raises engine.ChainFailed
+                            c.check_count(int(self.pin_state[slot][k]))
                         arr = self.pin_out[slot].numpy()
                         for i in range(n):
                             recorder.writeFrame(arr[i])
@@ -399,6 +407,8 @@ class VideoUpscaler:
                     self.h2d_done[slot].record(up.stream)
                 up.run_async()
                 with torch.cuda.stream(up.stream):
+                    for k, c in enumerate(self.chains):
+                        c.snapshot(self.pin_state[slot][k:k + 1])
                     self.pin_out[slot].copy_(up.bgr, non_blocking=True)
                     self.d2h_done[slot].record(up.stream)
                 q.put((slot, n))

@@ -343,7 +343,8 @@ int isr_conv3x3_check(const isr_conv_desc* d);
  * `state` (device, isr_conv_chain_state_words(n, ha, wa) uint32 words, zeroed ONCE by the
  * caller before first use, then owned by the library across calls: a generation counter in
  * state[0] replaces per-call zeroing); after a call, state[1] == state[0] means a dependency
- * wait gave up (results invalid — not expected unless the device is shared).  nl < 1024.
+ * wait gave up (results invalid — not expected unless the device is shared); state[2] counts
+ * give-ups over all launches (never reset: a host remembers the last count it saw).  nl < 1024.
  * acquire = 1 adds an agent-scope acquire before each tile's loads (otherwise the
  * hand-off relies on sc1 loads). */
 typedef struct isr_chain_desc {
@@ -362,7 +363,9 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
  * a bias, cin >= 64, r1 (if any) == the layer's own input with slope 1 and 1/s1 exact in bf16 —
  * a table that breaks this makes the launch give up: state[1] == state[0]); 1 = the round-2
  * kernel (conv3x3.hip: one independent conv tile per (layer, tile)).  Both produce the outputs
- * of the per-layer isr_conv3x3_fwd calls bit for bit. */
+ * of the per-layer isr_conv3x3_fwd calls bit for bit.  2 = trunk.hip in its two-workgroups-per-CU
+ * form (4 waves each, one K-chunk in flight; variant 0 runs one 8-wave workgroup per CU with three
+ * chunks in flight and two tiles of independent images interleaved per layer). */
 int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
 /* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
  * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,
@@ -372,6 +375,10 @@ int isr_tuning_trunk_stamps(void* buf);
  * bit 1 = no halo LDS-DMA after the first chunk, 2 = no MFMAs, 4 = no epilogue stores;
  * per_cu > 0 caps the resident workgroups per CU (the grid). */
 int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k3);
+/* Tuning builds only: per-item cycle stamps (s_memtime) of later production chain launches into
+ * `buf` (uint64 [grid][2 layers: 77, 79][16 items][2 waves][8]: item top, own DMA landed, barrier
+ * passed, refill issued, MFMAs issued) for each workgroup's first tile; NULL stops. */
+int isr_tuning_trunk_item_stamps(void* buf);
 
 int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s);
 int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);

@@ -63,7 +63,7 @@ def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks):
     gw = _gw(blocks)
     xs = _inputs(n, h, w, 3, seed=3)
     refs = _run(gw, xs, chain=False)
-    for variant in (0, 1):
+    for variant in (0, 2, 1):
         for acquire in (False, True):
             for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire, variant=variant), refs):
                 assert torch.equal(out, ref), \
@@ -116,8 +116,45 @@ def test_chain_poll_reports_a_give_up():
     torch.cuda.synchronize()
     plan.run(x, out)  # clean launches: no error
     torch.cuda.synchronize()
-    plan.chain.state[1] = plan.chain.state[0]  # as if the last launch's wait had given up
-    plan.chain._poll_host.copy_(plan.chain.state[:2])
+    plan.verify()
+    plan.chain.state[2] += 1  # as if a dependency wait had given up (the sticky give-up count)
     torch.cuda.synchronize()
     with pytest.raises(engine.ChainFailed):
         plan.run(x, out)
+        torch.cuda.synchronize()
+        plan.run(x, out)  # the lagged check raises on the call after the snapshot has landed
+    plan.chain.state[2] += 1
+    with pytest.raises(engine.ChainFailed):
+        plan.verify()  # the blocking check of one-shot consumers raises at once
+    plan.verify()      # reported once
+
+
+def test_give_up_raises_from_video_and_tiler_before_output():
+    """A give-up (simulated through the sticky count) must surface from the shipped consumers
+    BEFORE their outputs leave: the video writer (graph replays), FrameUpscaler's synchronous
+    call and the tiler's canvas."""
+    import numpy as np
+    from image_super_resolution_amd import tiler, video
+    gw = _gw(1, scale=2)
+    up = video.FrameUpscaler(gw, 24, 40, batch=2)
+    assert up.plan.chains, "the video plan must run the trunk on the persistent chain"
+    frames = [np.full((24, 40, 3), i, np.uint8) for i in range(5)]
+    rec = video.NullRecorder()
+    assert video.VideoUpscaler(up).run(frames, rec) == 5
+    up.plan.chain.state[2] += 1
+    rec = video.NullRecorder()
+    with pytest.raises(engine.ChainFailed):
+        video.VideoUpscaler(up).run(frames, rec)
+    assert rec.frames <= 2  # at most the batch in flight before the failing one was written
+    up.plan.chain.state[2] += 1
+    with pytest.raises(engine.ChainFailed):
+        up(torch.from_numpy(np.stack(frames[:2])))
+    runner = tiler.GeneratorRunner(gw, (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), DEV)
+    tu = tiler.TileUpscaler(runner, scale=2, window=32, halo=0, batch=4)
+    img = torch.randint(0, 255, (3, 40, 70), dtype=torch.uint8)
+    tu(img)
+    for plan in runner.plans.values():
+        for c in plan.chains:
+            c.state[2] += 1
+    with pytest.raises(engine.ChainFailed):
+        tu(img)

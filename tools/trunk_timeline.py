@@ -3,7 +3,7 @@
 ISR_LIB=.../libisr_tuning.so): stamps for the 15 layers of RRDB 5 (layers 75..89) —
 tile entry, chunk 0 landed, main loop done, stores issued, and (deferred refills only) the
 blocking dependency wait — as percentile rows in microseconds, plus the spacing of layer
-starts.  usage: python tools/trunk_timeline.py [acquire 0/1] [batch] [lr]"""
+starts.  usage: python tools/trunk_timeline.py [acquire 0/1] [batch] [lr] [variant 0/2]"""
 from __future__ import annotations
 
 import ctypes
@@ -26,6 +26,7 @@ def pct(v, qs=(0.1, 0.5, 0.9, 1.0)):
 def main():
     lib = _lib.load()
     acquire = bool(int(sys.argv[1])) if len(sys.argv) > 1 else False
+    engine.CHAIN_VARIANT = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     lrs = int(sys.argv[3]) if len(sys.argv) > 3 else 128
     dev = torch.device("cuda")
