@@ -117,7 +117,10 @@ struct C3 {
 __device__ __forceinline__ bf16x8 fold_a(float s1, int h16) {
     const __bf16 bi = (__bf16)(1.f / s1);
     const unsigned idv = __builtin_bit_cast(uint16_t, bi);
-    const int lane = threadIdx.x & 63;
+    int lane = threadIdx.x & 63;
+    // opaque to the optimiser: built next to its one use instead of hoisted out of the chunk
+    // loop (two hoisted operands = 8 VGPRs the 256-VGPR final-conv kernel does not have)
+    asm volatile("" : "+v"(lane));
     const int j = (lane & 31) - 16 * h16 - 8 * (lane >> 5);
     typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
     u32x4 r;

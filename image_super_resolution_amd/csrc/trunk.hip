@@ -517,8 +517,6 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     };
 
     f32x16 acc[R][NF];
-    bf16x8 q2[R][NF][2];
-    uint32_t r2_mark = 0;
 
     for (int ch = 0; ch < nch; ++ch, ++st.item) {
         const int slot = st.item % NST;
@@ -562,32 +560,6 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                 for (int r = 0; r < R; ++r) acc[r][f] = b0;
             }
         }
-        if (has_r2 && ch + 1 == nch) {
-            // RRDB residual of the epilogue, loaded now (older than the refill DMA below).  Ordinary
-            // (compiler-visible) loads: an asm load's destination may be copied or spilled by the
-            // register allocator before the data arrives; hipcc's own wait before their first use
-            // is at worst a full vmcnt(0), once per RRDB
-            const int xx = x0 + l31;
-            const uint32_t plane_px = (uint32_t)(c.hp * c.wp);
-            const uint32_t r2pl = (uint32_t)(img * c.cs16 + rec_r2p(rec)) * plane_px;
-            const auto rr = rsrc((const char*)(uintptr_t)rec.r2);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint32_t pix = (uint32_t)((y0 + wave * R + r + c.pad) * c.wp + xx + c.pad);
-#pragma unroll
-                for (int f = 0; f < NF; ++f)
-#pragma unroll
-                    for (int blk = 0; blk < 2; ++blk) {
-                        const int co = f * 32 + 16 * blk + 8 * hh;
-                        q2[r][f][blk] = __builtin_bit_cast(
-                            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                        rr, (r2pl + (uint32_t)(co >> 4) * plane_px + pix) * 32 + 16 * hh, 0, 16));
-                    }
-            }
-            st.issued += R * NF * 2;
-            r2_mark = st.issued;
-        }
-
         const char* sb = smem + slot * K::SLOT;
         bf16x8 fb[2][TN][NF], fa[2][NA];
         auto read_one = [&](int dx, int idx, int set) {
@@ -690,9 +662,30 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
         const bool scale2 = s2 != 1.f;
         const uint32_t plane_px = (uint32_t)(c.hp * c.wp);
         const uint32_t ypl = (uint32_t)(img * c.cs16 + rec_yp(rec)) * plane_px;
-        if (has_r2) wait_vm(st.issued - r2_mark);
+        // RRDB residual (every third RDB's final conv): row r + 1's values are loaded while row r
+        // is finished, so at most two rows (32 VGPRs) are live — loading them all before the last
+        // chunk's MFMAs (64 VGPRs beside the 128 accumulators and the fragments) spilled.
+        // Compiler-visible loads: hipcc places the wait before their first use itself.
+        bf16x8 q2[R][NF][2];
+        const uint32_t r2pl = (uint32_t)(img * c.cs16 + rec_r2p(rec)) * plane_px;
+        const auto rr = rsrc((const char*)(uintptr_t)rec.r2);
+        auto load_r2 = [&](int r) {
+            const uint32_t pix = (uint32_t)((y0 + wave * R + r + c.pad) * c.wp + xx + c.pad);
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    const int co = f * 32 + 16 * blk + 8 * hh;
+                    q2[r][f][blk] = __builtin_bit_cast(
+                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                    rr, (r2pl + (uint32_t)(co >> 4) * plane_px + pix) * 32 + 16 * hh, 0, 16));
+                }
+            st.issued += NF * 2;
+        };
+        if (has_r2) load_r2(0);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+            if (has_r2 && r + 1 < R) load_r2(r + 1);
             const int yy = y0 + wave * R + r;
             const bool valid = yy < c.h && xx < c.w;
             const uint32_t pix = (uint32_t)((yy + c.pad) * c.wp + xx + c.pad);
@@ -863,11 +856,15 @@ static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-using TK_DEEP = TK<8, 2, 4>;   // production: one 8-wave workgroup per CU, 3 chunks in flight
-using TK_PAIR = TK<4, 4, 2>;   // two 4-wave workgroups per CU, 1 chunk in flight
+// production: two 4-wave workgroups per CU, one chunk in flight (237 VGPRs, no scratch since
+// the RRDB residual is loaded row by row in the epilogue): 6.46 ms per bench forward against
+// 7.77 ms for the deep form (same box, tools/ab_chain.py, profiles/r03_ab_chain.jsonl) — the deep
+// form's 2-row waves read 7 LDS fragments per 6 MFMAs (4-row waves: 9 per 12)
+using TK_PAIR = TK<4, 4, 2>;
+using TK_DEEP = TK<8, 2, 4>;   // one 8-wave workgroup per CU, 3 chunks in flight
 
 int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
-    return form == 1 ? trunk_launch_k<TK_PAIR>(cd, s) : trunk_launch_k<TK_DEEP>(cd, s);
+    return form == 1 ? trunk_launch_k<TK_DEEP>(cd, s) : trunk_launch_k<TK_PAIR>(cd, s);
 }
 
 #ifdef ISR_TUNING

@@ -86,6 +86,47 @@ def shard_tiles(tiles: Sequence[Tile], world: int) -> list[list[Tile]]:
     return out
 
 
+def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | None = None) -> list[list[Tile]]:
+    """Multi-GPU deal of a still as horizontal bands: the image
+    splits into `world` x k full-width bands of equal core height (the last one ragged), each
+    extended by `halo` LR rows above and below (clipped to the image, like a window's halo);
+    rank r takes the k contiguous bands [r k, (r + 1) k).  k is the smallest count that keeps a
+    band's input within `max_rows` (the persistent trunk kernel's 2 GiB buffer window by
+    default, see band_max_rows).  Every band of a rank has one of at most two input shapes (an
+    interior band, an image-edge band), so a rank builds <= 2 plans and runs each band as ONE
+    batch-1 forward over the full width — instead of the 3-4 window shapes at batch 1-2 an LPT
+    deal of rs.py windows gives it, and with no vertical seams.  Returns per-rank Tile lists
+    (Tile.x = 0, Tile.w = width)."""
+    if world < 1 or halo < 0 or height < 1 or width < 1:
+        raise ValueError("plan_bands: world >= 1, halo >= 0 and a non-empty image required")
+    if max_rows is None:
+        max_rows = band_max_rows(width)
+    k = 1
+    while True:
+        core = -(-height // (world * k))
+        if core + 2 * halo <= max_rows or core == 1:
+            break
+        k += 1
+    bands: list[Tile] = []
+    for y in range(0, height, core):
+        h = min(core, height - y)
+        bands.append(Tile(len(bands), y, 0, h, width, max(0, y - halo), 0, min(height, y + h + halo), width))
+    out: list[list[Tile]] = [[] for _ in range(world)]
+    per = -(-len(bands) // world)
+    for b in bands:
+        out[min(world - 1, b.index // per)].append(b)
+    return out
+
+
+def band_max_rows(width: int, limit: int = 2 ** 31) -> int:
+    """Largest band input height whose 192-channel dense buffer (engine.GeneratorBuffers:
+    bf16, 16x32-rounded, 1-px border) stays below the trunk kernel's 2 GiB buffer window."""
+    from .ops import TILE_H, TILE_W, round_up
+    wa = round_up(width, TILE_W) + 2
+    rows = limit // (192 * 2 * wa) - 2
+    return max(TILE_H, rows // TILE_H * TILE_H - TILE_H)
+
+
 BatchRunner = Callable[[torch.Tensor], torch.Tensor]  # uint8 [b,3,h,w] → uint8 [b,3,s·h,s·w]
 
 
@@ -173,11 +214,26 @@ class TileUpscaler:
     """
 
     def __init__(self, runner: BatchRunner, scale: int, window: int = 96, halo: int = 0, batch: int = 8,
-                 device="cuda"):
+                 device="cuda", shard: str = "windows"):
+        """`shard` (world > 1 only): "windows" deals rs.py's windows longest-processing-time-first
+        (shard_tiles; the canvas equals the single-rank one bit for bit); "bands" gives every rank
+        full-width horizontal bands with the same halo (plan_bands; <= 2 plan shapes per rank, one
+        forward per band; needs halo > 0 to hide its seams, and differs from the windowed canvas
+        by the seams each form leaves)."""
         if batch < 1:
             raise ValueError("batch must be >= 1")
+        if shard not in ("windows", "bands"):
+            raise ValueError(f"shard must be 'windows' or 'bands', got {shard!r}")
         self.runner, self.scale, self.window, self.halo, self.batch = runner, scale, window, halo, batch
         self.device = torch.device(device)
+        self.shard = shard
+
+    def shards(self, height: int, width: int, world: int) -> list[list[Tile]]:
+        """The per-rank tile lists of an image (deterministic: every rank computes the same)."""
+        if world > 1 and self.shard == "bands":
+            return plan_bands(height, width, world, self.halo)
+        tiles = plan_tiles(height, width, self.window, self.halo)
+        return shard_tiles(tiles, world) if world > 1 else [tiles]
 
     def run_tiles(self, image: torch.Tensor, tiles: Sequence[Tile]) -> dict[int, torch.Tensor]:
         """Upscale `tiles` of `image` (uint8 [3,H,W] on self.device); returns
@@ -210,8 +266,9 @@ class TileUpscaler:
         c, H, W = image.shape
         s = self.scale
         image = image.to(self.device, non_blocking=True)
-        tiles = plan_tiles(H, W, self.window, self.halo)
-        mine = shard_tiles(tiles, world)[rank] if world > 1 else tiles
+        shards = self.shards(H, W, world)
+        tiles = [t for lst in shards for t in lst]
+        mine = shards[rank]
         done = self.run_tiles(image, mine)
         verify = getattr(self.runner, "verify", None)
         if verify is not None:
@@ -221,8 +278,7 @@ class TileUpscaler:
             for t in tiles:
                 canvas[:, t.y * s:(t.y + t.h) * s, t.x * s:(t.x + t.w) * s] = done[t.index]
             return canvas
-        return _gather_to_rank0(tiles, shard_tiles(tiles, world), done, s, (c, H * s, W * s), rank, group,
-                                self.device)
+        return _gather_to_rank0(tiles, shards, done, s, (c, H * s, W * s), rank, group, self.device)
 
 
 def _gather_to_rank0(tiles, shards, done, s, canvas_shape, rank, group, device):

@@ -317,6 +317,7 @@ class GeneratorTrainPlan:
             bn_bwd(c, self.Tz, self.gT, dz=self.gtmp)
             g1 = self.gtmp
         wg3(D[-1], 64, g1, 64, c)
+        B.append(("ready", "tail", False))  # conv1 / Scaler / tail gradients complete (main stream)
         B.append(("conv", ops.conv3x3_desc(g1, 64, c.bwd, None, 64, U)))
         # RRDBs, reverse
         nb = len(self.rdbs) // 3
@@ -346,10 +347,16 @@ class GeneratorTrainPlan:
                     wg3(Dj, 192, E, 64, cs[4], scale=a * res, side=True)
                     for t in range(3, -1, -1):
                         wg3(Dj, cs[t].cin, E, 32, cs[t], g_coff=64 + 32 * (3 - t), side=True)
+                    if step == 2:  # RRDB i's weight gradients are all enqueued (side stream)
+                        B.append(("ready", i, True))
                     # v = (acc / res + g_out) * res (+ g_R: the RRDB's own residual, first RDB)
                     kw = dict(r2=self.Eg[3 * i + 2]) if step == 2 else {}
+                    # r1_cn=64 (= every output channel, the same sums) keeps this conv on the plain
+                    # 192->64 kernel: with r1 aliasing x, cout 64 and 1/s1 exact (res = 1) libisr
+                    # would pick the residual-fold form the inference trunk needs for bit-identity,
+                    # which costs the per-conv kernel registers (scratch spills)
                     B.append(("conv", ops.conv3x3_desc(E, 192, gp["x"], None, 64, gout, r1=E, s1=1.0 / res, s2=res,
-                                                       **kw)))
+                                                       r1_cn=64, **kw)))
             U = self.gtrunk
         for i in range(nb - 1, -1, -1) if not self.gather else ():
             # g_R (gradient wrt the RRDB output) is in U[0:64]
@@ -382,6 +389,7 @@ class GeneratorTrainPlan:
                         kw = dict(r2=U, s2=1.0)  # + g_R: the RRDB's own residual
                     B.append(("conv", ops.conv3x3_desc(gout, 32, ck.bwd, None, ck.cin, gout, x_coff=slot,
                                                        r1=gout, **kw)))
+            B.append(("ready", i, False))  # RRDB i's gradients complete (main stream)
             # RRDB input gradient now in V[0:64]; rotate so it becomes the next g_R
             U, V, W = V, W, U
         # trunk: g_f0 = chain + g_T, then LeakyReLU'(f0) of conv0
@@ -389,6 +397,7 @@ class GeneratorTrainPlan:
                                             mslope=self.slope0)))
         d9h = ops.wgrad9x9_desc(self.dummy_x, self.gf0, _meta_dw(64, 3, 9, dev), None, head=True)
         B.append(("wg9", d9h, ci[id(self.head)]))
+        B.append(("ready", "head", False))
         self.bwd_launches = B
         self.head_wg = d9h
         # workspace for the split-K partial sums
@@ -423,6 +432,15 @@ class GeneratorTrainPlan:
                 go, bo2 = self._goff[pi], self._goff[pi + 1]
                 pi += 2
             self._conv_goff.append((wo, bo, go, bo2))
+        # data-parallel gradient buckets: the flat buffer in backward order is
+        # [conv1 .. tail] (end of the buffer), RRDB nb-1, ..., RRDB 0, head (start) — contiguous
+        # descending ranges, each complete at its ("ready", id) entry of the backward list
+        first = lambda conv_index: self._conv_goff[conv_index][0]
+        nr = len(self.rdbs)
+        seg = {"tail": (first(1 + 5 * nr), self._gsize), "head": (0, first(1) if nr else self._gsize)}
+        for i in range(nr // 3):
+            seg[i] = (first(1 + 15 * i), first(1 + 15 * (i + 1)))
+        self._segments = seg
 
     # -------------------------------------------------------------- execution
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -469,8 +487,14 @@ class GeneratorTrainPlan:
         if self.side is not None:
             self.side.wait_stream(main)  # `grads` and the forward's activations are ready
             sst = ctypes.c_void_p(self.side.cuda_stream)
+        group = self.gen.__dict__.get("_isr_grad_group")
+        ddp = _Buckets(self, grads, group, main) if group is not None else None
         for e in self.bwd_launches:
             kind, d = e[0], e[1]
+            if kind == "ready":
+                if ddp is not None:
+                    ddp.ready(d, self.side if (e[2] and self.side is not None) else main)
+                continue
             if kind in ("evrec", "evwait") and self.side is None:
                 continue
             if kind == "evrec":
@@ -508,18 +532,67 @@ class GeneratorTrainPlan:
                 ops.check(rc, f"train backward ({kind})")
         if side_used:
             main.wait_stream(self.side)
-        group = self.gen.__dict__.get("_isr_grad_group")
-        if group is not None:
-            # data-parallel: one RCCL all-reduce of the whole flat gradient buffer
-            # (47.5 MB for the 16-block generator) instead of DDP's per-bucket hooks
-            import torch.distributed as dist
-            g = group if group is not True else None
-            all_reduce_(grads, g)
-            grads.div_(dist.get_world_size(g))
+        if ddp is not None:
+            ddp.finish()  # the main stream waits for every bucket, then the mean
         out = []
         for p, off in zip(self._params, self._goff):
             out.append(grads[off:off + p.numel()].view(p.shape))
         return out
+
+
+# DDP-style gradient buckets: consecutive backward segments are merged until a bucket holds at
+# least this many bytes (xGMI rings are per-link bound: a few MB per call keeps the fixed cost
+# per collective small against its transfer time; 47.5 MB of generator gradients -> ~6 buckets)
+BUCKET_BYTES = int(float(_os.environ.get("ISR_DDP_BUCKET_MB", "8")) * (1 << 20))
+
+
+class _Buckets:
+    """The data-parallel gradient all-reduce of one backward, overlapped with it (SURVEY.md §8e,
+    DDP's bucketed all-reduce): the flat fp32 gradient buffer's segments complete in backward
+    order (tail, RRDB nb-1 .. 0, head); consecutive segments merge into buckets of >=
+    BUCKET_BYTES, and each bucket is all-reduced on a communication stream as soon as the stream
+    that produced its last segment (main, or the side stream of the RDB weight gradients) has
+    enqueued it — an event hand-off, no host synchronisation.  finish() makes the main stream
+    wait for every bucket and divides by the world size.  Same sums as one flat all-reduce per
+    element (each element is reduced exactly once), so ranks stay bitwise equal."""
+
+    def __init__(self, plan, grads: torch.Tensor, group, main):
+        import torch.distributed as dist
+        self.dist, self.plan, self.grads, self.main = dist, plan, grads, main
+        self.group = None if group is True else group
+        self.comm = plan.__dict__.setdefault("_comm_stream", torch.cuda.Stream(grads.device))
+        self.lo = self.hi = None
+        self.works = []
+
+    def ready(self, seg_id, stream) -> None:
+        lo, hi = self.plan._segments[seg_id]
+        if self.hi is None:
+            self.lo, self.hi = lo, hi
+        else:
+            assert hi == self.lo, "gradient segments must complete in descending buffer order"
+            self.lo = lo
+        if (self.hi - self.lo) * 4 >= BUCKET_BYTES or seg_id == "head":
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                self._reduce(self.grads[self.lo:self.hi])
+            self.lo = self.hi = None
+
+    def _reduce(self, t: torch.Tensor) -> None:
+        dist = self.dist
+        if dist.get_backend(self.group) == "gloo":  # host-staged (rehearsal on one GPU, tests)
+            all_reduce_(t, self.group)
+        else:
+            self.works.append(dist.all_reduce(t, group=self.group, async_op=True))
+
+    def finish(self) -> None:
+        if self.hi is not None:
+            raise RuntimeError("gradient buckets: the backward ended with an unreduced segment")
+        for w in self.works:
+            w.wait()  # the current (main) stream waits for the collective
+        self.main.wait_stream(self.comm)
+        self.grads.div_(self.dist.get_world_size(self.group))
 
 
 def _meta_dw(cout: int, cin: int, k: int, dev) -> torch.Tensor:
@@ -558,8 +631,9 @@ def verify_chains(gen: nn.Module) -> None:
     generator (engine.ChainFailed); the trainer calls it at the end of every epoch, before the
     epoch's results (losses, checkpoint) are handed out."""
     plan = gen.__dict__.get("_isr_train_plan")
-    if plan is not None and plan.chain is not None:
-        plan.chain.verify()
+    chain = getattr(plan, "chain", None)  # the Denoise training plan has no trunk chain
+    if chain is not None:
+        chain.verify()
 
 
 def get_train_plan(gen: nn.Module, x: torch.Tensor) -> GeneratorTrainPlan:

@@ -363,9 +363,9 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
  * a bias, cin >= 64, r1 (if any) == the layer's own input with slope 1 and 1/s1 exact in bf16 —
  * a table that breaks this makes the launch give up: state[1] == state[0]); 1 = the round-2
  * kernel (conv3x3.hip: one independent conv tile per (layer, tile)).  Both produce the outputs
- * of the per-layer isr_conv3x3_fwd calls bit for bit.  2 = trunk.hip in its two-workgroups-per-CU
- * form (4 waves each, one K-chunk in flight; variant 0 runs one 8-wave workgroup per CU with three
- * chunks in flight and two tiles of independent images interleaved per layer). */
+ * of the per-layer isr_conv3x3_fwd calls bit for bit.  0 = trunk.hip in its two-workgroups-per-CU
+ * form (4 waves of 4 output rows each, one K-chunk in flight); 2 = trunk.hip with one 8-wave
+ * workgroup per CU (2 output rows per wave) and three chunks in flight. */
 int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
 /* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
  * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,

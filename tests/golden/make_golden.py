@@ -231,9 +231,10 @@ def golden_disc(M):
     """11. Discriminator(3, 64, 8, 1024) (utils/models.py:513-569) in train mode, fp32,
     as SRGAN training runs it (train.py:307, :113-126): logits for a [4,3,64,64]
     input, then backward of sum(logits * w) — input gradient, every parameter
-    gradient (tensors above 16384 elements: their first 16384 flattened elements,
-    to keep the fixture small), and the BatchNorm running statistics after that
-    forward."""
+    gradient (tensors above 16384 elements: 16384 flattened elements drawn uniformly
+    over the WHOLE tensor, sorted, their indices stored as `gidx:{name}` — a sample of
+    every output channel and tap, not just the first rows), and the BatchNorm running
+    statistics after that forward."""
     torch.manual_seed(0)
     model = load_synth(M.Discriminator(3, 64, 8, 1024), 40).train()
     g = torch.Generator().manual_seed(41)
@@ -243,8 +244,14 @@ def golden_disc(M):
         y = model(x)
         (y * w).sum().backward()
     out = dict(x=np32(x), w=np32(w), y=np32(y), dx=np32(x.grad), seed=40)
+    gs = torch.Generator().manual_seed(42)
     for k, p in model.named_parameters():
-        out[f"grad:{k}"] = np32(p.grad.flatten()[:16384])
+        flat = p.grad.flatten()
+        if flat.numel() > 16384:
+            idx = torch.randperm(flat.numel(), generator=gs)[:16384].sort().values
+            out[f"gidx:{k}"] = idx.to(torch.int32).numpy()
+            flat = flat[idx]
+        out[f"grad:{k}"] = np32(flat)
     for k, b in model.named_buffers():
         if "running" in k:
             out[f"stat:{k}"] = np32(b)

@@ -73,6 +73,36 @@ def test_shard_lpt_balanced_and_complete():
         assert max(loads) - min(loads) <= max(t.cost for t in tiles)
 
 
+@pytest.mark.parametrize("h,w,world,halo,max_rows", [(2160, 3840, 8, 32, None), (45, 61, 2, 2, None),
+                                                      (45, 61, 3, 1, 8), (5, 9, 8, 1, None), (100, 7, 4, 0, 12)])
+def test_plan_bands_cover_and_shapes(h, w, world, halo, max_rows):
+    """Bands cover every image row once, in order; each rank holds <= 2 input shapes, every
+    band fits max_rows, the halo is clipped to the image."""
+    shards = tiler.plan_bands(h, w, world, halo, max_rows)
+    assert len(shards) == world
+    bands = [b for s in shards for b in s]
+    assert [b.index for b in bands] == list(range(len(bands)))
+    rows = [r for b in bands for r in range(b.y, b.y + b.h)]
+    assert rows == list(range(h))
+    for b in bands:
+        assert (b.x, b.w, b.x0, b.x1) == (0, w, 0, w)
+        assert b.y0 == max(0, b.y - halo) and b.y1 == min(h, b.y + b.h + halo)
+        if max_rows is not None and b.h > 1:
+            assert b.y1 - b.y0 <= max_rows
+    for s in shards:
+        assert len({b.in_shape for b in s}) <= 2
+
+
+def test_plan_bands_cfg4_one_plan_per_rank():
+    """cfg4 (3840x2160, halo 32) over 8 ranks: one band per rank (270 core rows), two input
+    shapes in all (edge 302 rows, interior 334), below the trunk kernel's 2 GiB window."""
+    shards = tiler.plan_bands(2160, 3840, 8, 32)
+    assert [len(s) for s in shards] == [1] * 8
+    assert sorted({s[0].in_shape for s in shards}) == [(302, 3840), (334, 3840)]
+    assert tiler.band_max_rows(3840) >= 334
+    assert 192 * 2 * (336 + 2) * (3840 + 2) < 2 ** 31
+
+
 def test_runner_shape_check():
     up = tiler.TileUpscaler(lambda x: x, S, window=8, device="cpu")
     with pytest.raises(RuntimeError, match="runner returned"):
@@ -85,12 +115,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, shard="windows"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         img = image(45, 61, seed=11)
-        up = tiler.TileUpscaler(box_up, S, window=16, halo=2, batch=2, device="cpu")
+        up = tiler.TileUpscaler(box_up, S, window=16, halo=2, batch=2, device="cpu", shard=shard)
         out = up(img, rank=rank, world=world)
         if rank == 0:
             q.put(out.numpy())  # by value: a shared-memory tensor handle can vanish when this rank exits
@@ -100,11 +130,14 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_gloo_world2_matches_single():
+@pytest.mark.parametrize("shard", ["windows", "bands"])
+def test_sharded_gloo_world2_matches_single(shard):
+    """2 ranks over gloo: the canvas rank 0 stitches equals the single-rank one (halo 2 >= the
+    operator's radius, so the bands deal gives the same whole-image result as windows)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shard)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(2)]

@@ -8,7 +8,13 @@ longest-processing-time-first over the ranks (tiler.shard_tiles, no data-path
 collective), rank 0 receives finished tiles point-to-point and owns the canvas.
 Reports HR megapixels/s of the whole image (after one warm-up call that builds
 the plans), seconds per image, and peak device memory.
-usage: python tools/bench_still.py [--reps 3] [--batch 4] [--halo 32]
+
+--sim-world N (one GPU, no torch.distributed): predicts the N-GPU wall time.  After the
+1-GPU windowed run (t1), every rank's share of an N-rank deal (--shard windows: the LPT deal of
+rs.py windows; bands: tiler.plan_bands) runs alone on this GPU, timed like the real run
+(same plans, median of --reps); the predicted N-GPU time is the slowest rank's, reported
+against t1 / N.  The point-to-point gather of finished tiles to rank 0 is not included.
+usage: python tools/bench_still.py [--reps 3] [--batch 4] [--halo 32] [--shard bands] [--sim-world 8]
 """
 from __future__ import annotations
 
@@ -38,6 +44,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--shard", default="windows", choices=("windows", "bands"))
+    ap.add_argument("--sim-world", type=int, default=0)
     args = ap.parse_args()
     world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
@@ -55,7 +63,8 @@ def main():
     img = torch.nn.functional.interpolate(lo, size=(args.height, args.width), mode="bicubic")
     img = (img.clamp(0, 1)[0] * 255).round().to(torch.uint8)
     runner = tiler.runner_for(model, dev)
-    up = tiler.TileUpscaler(runner, 4, window=args.window, halo=args.halo, batch=args.batch, device=dev)
+    up = tiler.TileUpscaler(runner, 4, window=args.window, halo=args.halo, batch=args.batch, device=dev,
+                            shard=args.shard)
     torch.cuda.reset_peak_memory_stats(dev)
     with torch.no_grad():
         t0 = time.perf_counter()
@@ -89,12 +98,42 @@ def main():
            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
            "plans_cached": len(runner.plans), "plan_cache_gib": round(runner.cached_bytes() / 2**30, 2),
            "canvas": list(canvas.shape) if canvas is not None else None}
+    if args.sim_world > 1 and world == 1:
+        res.update(simulate(args, up, runner, img.to(dev), t, dev))
     if rank == 0:
         print(json.dumps(res), flush=True)
         if args.out:
             Path(args.out).write_text(json.dumps(res, indent=1))
     if world > 1:
         dist.destroy_process_group()
+
+
+def simulate(args, up, runner, img, t1, dev):
+    """Each rank's share of an args.sim_world deal run alone on this GPU (see module doc)."""
+    N = args.sim_world
+    shards = up.shards(img.shape[1], img.shape[2], N)
+    ranks = []
+    with torch.no_grad():
+        for r in range(N):
+            up.run_tiles(img, shards[r])  # warm: builds this rank's plans
+            runner.verify()
+            ts = []
+            for _ in range(args.reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                up.run_tiles(img, shards[r])
+                runner.verify()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            shapes = sorted({tt.in_shape for tt in shards[r]})
+            ranks.append({"rank": r, "s": round(statistics.median(ts), 4), "tiles": len(shards[r]),
+                          "shapes": shapes, "run_px": sum(tt.cost for tt in shards[r])})
+            print(json.dumps({"sim_rank": ranks[-1]}), flush=True)
+    mx = max(x["s"] for x in ranks)
+    return {"sim_world": N, "shard": args.shard, "sim_ranks": ranks, "sim_max_rank_s": mx,
+            "sim_t1_over_n_s": round(t1 / N, 4), "sim_ratio": round(mx / (t1 / N), 3),
+            "sim_value_mpix_s": round(args.height * args.width * 16 / mx / 1e6, 1),
+            "sim_note": "per-rank shares run alone on one GPU; gather to rank 0 excluded"}
 
 
 if __name__ == "__main__":
