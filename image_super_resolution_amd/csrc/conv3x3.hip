@@ -112,11 +112,15 @@ struct C3 {
     static_assert(KC == 16 || KC == 32, "chunk width");
 };
 
+template <int V> struct IC { static constexpr int value = V; };
+
 // A operand of the residual fold: (1/s1) I on couts [16 h16, 16 h16 + 16) of a 32-cout
 // fragment (lane l supplies A[l & 31][8 (l >> 5) .. + 8]); trunk.hip builds the same.
-__device__ __forceinline__ bf16x8 fold_a(float s1, int h16) {
+__device__ __forceinline__ uint32_t fold_idv(float s1) {  // bf16 bits of 1/s1, in an SGPR
     const __bf16 bi = (__bf16)(1.f / s1);
-    const unsigned idv = __builtin_bit_cast(uint16_t, bi);
+    return __builtin_amdgcn_readfirstlane((uint32_t)__builtin_bit_cast(uint16_t, bi));
+}
+__device__ __forceinline__ bf16x8 fold_a(uint32_t idv, int h16) {
     int lane = threadIdx.x & 63;
     // opaque to the optimiser: built next to its one use instead of hoisted out of the chunk
     // loop (two hoisted operands = 8 VGPRs the 256-VGPR final-conv kernel does not have)
@@ -328,6 +332,7 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
     // (A = (1/s1) I, exact in bf16) and the epilogue computes acc * s1 — no r1 re-read.  The
     // same MFMA order as trunk.hip's kernel, so every path stays bit-identical.
     const bool fold = fold_ok<C, XS2>(d);
+    const uint32_t fidv = C::FOLD ? fold_idv(d.s1) : 0u;
     conv_stamp(0, srow);
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
@@ -445,165 +450,181 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
     conv_stamp(5, srow);
 
     const int qw = wave * R * C::HC + l31; // halo pixel of (row w*R, col l31)
-    for (int chunk = 0; chunk < nchunks; ++chunk) {
-        // chunk `chunk` landed for this wave: younger chunks in flight = min(NST-2, nchunks-1-chunk)
-        if constexpr (C::NSW) {
-            // issue order ... w(c-1) h(c+1) | w(c) h(c+2) ...: at chunk c only the halo pieces of
-            // chunk c+1 (issued after w(c)) may still be in flight (NST == 3)
-            static_assert(C::NSW == 0 || C::NST == 3, "split-ring wait assumes NST 3");
-            if (chunk + 1 < nchunks) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::IPWH) : "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        } else if constexpr (C::NST >= 3) {
-            if (chunk + C::NST - 2 < nchunks) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((C::NST - 2) * C::IPW) : "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (chunk == 0) conv_stamp(1, srow);
-        const bool refill = !(C::ABL & 2) && chunk + C::NST - 1 < nchunks;
-        // split rings: w(chunk+1) then h(chunk+NST-1), each when it exists
-        auto refill_split = [&]() {
-            if (chunk + 1 < nchunks) stage_w(chunk + 1, (chunk + 1) % C::NSW);
-            if (refill) stage_h(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
-        };
-        if constexpr (C::SPL == 1 || (C::SPL == 0 && C::PIPE != 2)) {
-            if constexpr (C::NSW) refill_split();
-            else if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
-        }
-
-        const char* hs = C::NSW ? smem + (chunk % C::NST) * C::HSTAGE
-                                : smem + ((C::ABL & 2) ? 0 : (chunk % C::NST)) * C::STAGE;
-        const char* ws = C::NSW ? smem + C::NST * C::HSTAGE + (chunk % (C::NSW ? C::NSW : 1)) * C::WSTAGE
-                                : hs + C::HALO_INSTR * 1024;
-        // Software pipeline over the chunk's (k-step, dx) steps: the fragments of
-        // step st+1 are read into the other register set while step st's MFMAs
-        // run, so LDS latency is covered by MFMA work of the same wave.
-        constexpr int NS = C::KS * C::TN;
-        constexpr int TN = C::TN, TLO = C::TLO, NA = C::NA;
-        bf16x8 fb[2][TN][NF], fa[2][NA];
-        auto load_step = [&](int st, int set) {
-            const int ks = st / TN, dx = TLO + st % TN;
-            const char* hp = hs + ks * C::HIPL * 1024;
-#pragma unroll
-            for (int dyi = 0; dyi < TN; ++dyi)
-#pragma unroll
-                for (int f = 0; f < NF; ++f) {
-                    const int n = f * 32 + l31;
-                    const int u = ((ks * 9 + (TLO + dyi) * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
-                    fb[set][dyi][f] = lds_read16(ws + u * 16);
+    // one K-chunk; FC = the chunk index (0..3) when the residual fold adds its MFMAs to this chunk,
+    // -1 otherwise (the fold's chunks are peeled so that its accumulator choice is compile-time:
+    // a run-time choice made hipcc copy a 16-VGPR accumulator and spill the 192->64 kernel)
+    auto do_chunk = [&](const int chunk, auto fc_tag) {
+        constexpr int FC = decltype(fc_tag)::value;
+        (void)FC;
+            // chunk `chunk` landed for this wave: younger chunks in flight = min(NST-2, nchunks-1-chunk)
+            if constexpr (C::NSW) {
+                // issue order ... w(c-1) h(c+1) | w(c) h(c+2) ...: at chunk c only the halo pieces of
+                // chunk c+1 (issued after w(c)) may still be in flight (NST == 3)
+                static_assert(C::NSW == 0 || C::NST == 3, "split-ring wait assumes NST 3");
+                if (chunk + 1 < nchunks) {
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::IPWH) : "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
-#pragma unroll
-            for (int ia = 0; ia < NA; ++ia) {
-                const int q = qw + (TLO + ia) * C::HC + dx;
-                fa[set][ia] = lds_read16(hp + halo_unit2(q, hh) * 16);
-            }
-        };
-        // one fragment of step st: idx < TN*NF → weights (dyi, f), else activation row ia
-        auto read_one = [&](int st, int idx, int set) {
-            const int ks = st / TN, dx = TLO + st % TN;
-            if (idx < TN * NF) {
-                const int dyi = idx / NF, f = idx % NF;
-                const int n = f * 32 + l31;
-                const int u = ((ks * 9 + (TLO + dyi) * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
-                fb[set][dyi][f] = lds_read16(ws + u * 16);
+            } else if constexpr (C::NST >= 3) {
+                if (chunk + C::NST - 2 < nchunks) {
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((C::NST - 2) * C::IPW) : "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             } else {
-                const int ia = idx - TN * NF;
-                const int q = qw + (TLO + ia) * C::HC + dx;
-                fa[set][ia] = lds_read16(hs + ks * C::HIPL * 1024 + halo_unit2(q, hh) * 16);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-        };
-        if constexpr (C::PIPE) load_step(0, 0);
-        if constexpr (C::PIPE == 2) {
-            // the refill's LDS-DMA issue (10-16 instructions, scalar address math) runs while
-            // step 0's fragment reads are in flight, instead of ahead of them
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (C::SPL == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (chunk == 0) conv_stamp(1, srow);
+            const bool refill = !(C::ABL & 2) && chunk + C::NST - 1 < nchunks;
+            // split rings: w(chunk+1) then h(chunk+NST-1), each when it exists
+            auto refill_split = [&]() {
+                if (chunk + 1 < nchunks) stage_w(chunk + 1, (chunk + 1) % C::NSW);
+                if (refill) stage_h(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+            };
+            if constexpr (C::SPL == 1 || (C::SPL == 0 && C::PIPE != 2)) {
                 if constexpr (C::NSW) refill_split();
                 else if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
             }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int st = 0; st < NS; ++st) {
-            const int cur = C::PIPE ? (st & 1) : 0;
-            if constexpr (C::SPL > 1) {
-                static_assert(C::SPL <= NS, "refill parts must fit the chunk's steps");
-                if (st < C::SPL && refill)
-                    stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST, st * C::IPW / C::SPL,
-                          (st + 1) * C::IPW / C::SPL);
-            }
-            if constexpr (C::PIPE == 2) {
-                // interleaved: this step's MFMAs with the next step's fragment reads (one
-                // read after each MFMA), so at most one step's reads are in flight (<= 15,
-                // the lgkmcnt range: beyond it hipcc can only wait lgkmcnt(0))
-                constexpr int NRD = TN * NF + NA;  // reads per step
-                constexpr int NM = R * TN * NF;    // MFMAs per step
-                int m = 0;
 
-#pragma unroll
+            const char* hs = C::NSW ? smem + (chunk % C::NST) * C::HSTAGE
+                                    : smem + ((C::ABL & 2) ? 0 : (chunk % C::NST)) * C::STAGE;
+            const char* ws = C::NSW ? smem + C::NST * C::HSTAGE + (chunk % (C::NSW ? C::NSW : 1)) * C::WSTAGE
+                                    : hs + C::HALO_INSTR * 1024;
+            // Software pipeline over the chunk's (k-step, dx) steps: the fragments of
+            // step st+1 are read into the other register set while step st's MFMAs
+            // run, so LDS latency is covered by MFMA work of the same wave.
+            constexpr int NS = C::KS * C::TN;
+            constexpr int TN = C::TN, TLO = C::TLO, NA = C::NA;
+            bf16x8 fb[2][TN][NF], fa[2][NA];
+            auto load_step = [&](int st, int set) {
+                const int ks = st / TN, dx = TLO + st % TN;
+                const char* hp = hs + ks * C::HIPL * 1024;
+    #pragma unroll
+                for (int dyi = 0; dyi < TN; ++dyi)
+    #pragma unroll
+                    for (int f = 0; f < NF; ++f) {
+                        const int n = f * 32 + l31;
+                        const int u = ((ks * 9 + (TLO + dyi) * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
+                        fb[set][dyi][f] = lds_read16(ws + u * 16);
+                    }
+    #pragma unroll
                 for (int ia = 0; ia < NA; ++ia) {
-#pragma unroll
+                    const int q = qw + (TLO + ia) * C::HC + dx;
+                    fa[set][ia] = lds_read16(hp + halo_unit2(q, hh) * 16);
+                }
+            };
+            // one fragment of step st: idx < TN*NF → weights (dyi, f), else activation row ia
+            auto read_one = [&](int st, int idx, int set) {
+                const int ks = st / TN, dx = TLO + st % TN;
+                if (idx < TN * NF) {
+                    const int dyi = idx / NF, f = idx % NF;
+                    const int n = f * 32 + l31;
+                    const int u = ((ks * 9 + (TLO + dyi) * 3 + dx) * C::CT + n) * 2 + (hh ^ ((n >> 3) & 1));
+                    fb[set][dyi][f] = lds_read16(ws + u * 16);
+                } else {
+                    const int ia = idx - TN * NF;
+                    const int q = qw + (TLO + ia) * C::HC + dx;
+                    fa[set][ia] = lds_read16(hs + ks * C::HIPL * 1024 + halo_unit2(q, hh) * 16);
+                }
+            };
+            if constexpr (C::PIPE) load_step(0, 0);
+            if constexpr (C::PIPE == 2) {
+                // the refill's LDS-DMA issue (10-16 instructions, scalar address math) runs while
+                // step 0's fragment reads are in flight, instead of ahead of them
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (C::SPL == 0) {
+                    if constexpr (C::NSW) refill_split();
+                    else if (refill) stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+    #pragma unroll
+            for (int st = 0; st < NS; ++st) {
+                const int cur = C::PIPE ? (st & 1) : 0;
+                if constexpr (C::SPL > 1) {
+                    static_assert(C::SPL <= NS, "refill parts must fit the chunk's steps");
+                    if (st < C::SPL && refill)
+                        stage(chunk + C::NST - 1, (chunk + C::NST - 1) % C::NST, st * C::IPW / C::SPL,
+                              (st + 1) * C::IPW / C::SPL);
+                }
+                if constexpr (C::PIPE == 2) {
+                    // interleaved: this step's MFMAs with the next step's fragment reads (one
+                    // read after each MFMA), so at most one step's reads are in flight (<= 15,
+                    // the lgkmcnt range: beyond it hipcc can only wait lgkmcnt(0))
+                    constexpr int NRD = TN * NF + NA;  // reads per step
+                    constexpr int NM = R * TN * NF;    // MFMAs per step
+                    int m = 0;
+
+    #pragma unroll
+                    for (int ia = 0; ia < NA; ++ia) {
+    #pragma unroll
+                        for (int dyi = 0; dyi < TN; ++dyi) {
+                            const int r = ia - dyi;
+                            if (r >= 0 && r < R) {
+    #pragma unroll
+                                for (int f = 0; f < NF; ++f) {
+                                    acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
+                                    if (st + 1 < NS)
+                                        for (int k = m * NRD / NM; k < (m + 1) * NRD / NM; ++k) read_one(st + 1, k, cur ^ 1);
+                                    __builtin_amdgcn_sched_barrier(0);  // pin the (MFMA, reads) order
+                                    ++m;
+                                }
+                            }
+                        }
+                        if constexpr (FC >= 0 && C::FOLD && C::NF == 2 && C::KS == 1 && C::TN == 3) {
+                            // residual fold: + x/s1 on the centre pixels of output row ia - 1 (dx = 1,
+                            // dy = 1), right after input row ia's MFMAs (trunk.hip's order); the chunk
+                            // (0..3) is a compile-time constant here, so the target accumulator is too
+                            if (st == 1 && ia >= 1 && ia <= R) {
+                                const bf16x8 a = fold_a(fidv, FC & 1);
+                                acc[ia - 1][FC >> 1] = mfma32(a, fa[cur][ia], acc[ia - 1][FC >> 1]);
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                        }
+                    }
+                    continue;
+                } else if constexpr (C::PIPE) {
+                    if (st + 1 < NS) load_step(st + 1, cur ^ 1);
+                    // keep the prefetch ahead of this step's MFMAs (hipcc otherwise sinks
+                    // each ds_read next to its first use and waits lgkmcnt(0) there)
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+                    load_step(st, 0);
+                }
+                // input row TLO+ia feeds output row r through kernel row dy = TLO+dyi: r = ia - dyi
+    #pragma unroll
+                for (int ia = 0; ia < NA; ++ia) {
+    #pragma unroll
                     for (int dyi = 0; dyi < TN; ++dyi) {
                         const int r = ia - dyi;
                         if (r >= 0 && r < R) {
-#pragma unroll
+    #pragma unroll
                             for (int f = 0; f < NF; ++f) {
-                                acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
-                                if (st + 1 < NS)
-                                    for (int k = m * NRD / NM; k < (m + 1) * NRD / NM; ++k) read_one(st + 1, k, cur ^ 1);
-                                __builtin_amdgcn_sched_barrier(0);  // pin the (MFMA, reads) order
-                                ++m;
-                            }
-                        }
-                    }
-                    if constexpr (C::FOLD && C::NF == 2 && C::KS == 1 && C::TN == 3) {
-                        // residual fold: + x/s1 on the centre pixels of output row ia - 1 (dx = 1,
-                        // dy = 1), right after input row ia's MFMAs (trunk.hip's order)
-                        if (st == 1 && fold && chunk < 4 && ia >= 1 && ia <= R) {
-                            const bf16x8 a = fold_a(d.s1, chunk & 1);
-                            if (chunk < 2) acc[ia - 1][0] = mfma32(a, fa[cur][ia], acc[ia - 1][0]);
-                            else acc[ia - 1][1] = mfma32(a, fa[cur][ia], acc[ia - 1][1]);
-                            __builtin_amdgcn_sched_barrier(0);
-                        }
-                    }
-                }
-                continue;
-            } else if constexpr (C::PIPE) {
-                if (st + 1 < NS) load_step(st + 1, cur ^ 1);
-                // keep the prefetch ahead of this step's MFMAs (hipcc otherwise sinks
-                // each ds_read next to its first use and waits lgkmcnt(0) there)
-                __builtin_amdgcn_sched_barrier(0);
-            } else {
-                load_step(st, 0);
-            }
-            // input row TLO+ia feeds output row r through kernel row dy = TLO+dyi: r = ia - dyi
-#pragma unroll
-            for (int ia = 0; ia < NA; ++ia) {
-#pragma unroll
-                for (int dyi = 0; dyi < TN; ++dyi) {
-                    const int r = ia - dyi;
-                    if (r >= 0 && r < R) {
-#pragma unroll
-                        for (int f = 0; f < NF; ++f) {
-                            if constexpr (C::ABL & 1) {
-                                asm volatile("" ::"v"(fa[cur][ia]), "v"(fb[cur][dyi][f]));
-                            } else {
-                                acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
+                                if constexpr (C::ABL & 1) {
+                                    asm volatile("" ::"v"(fa[cur][ia]), "v"(fb[cur][dyi][f]));
+                                } else {
+                                    acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
+                                }
                             }
                         }
                     }
                 }
             }
+    };
+    int chunk0 = 0;
+    if constexpr (C::FOLD && C::NF == 2 && C::KS == 1 && C::TN == 3) {
+        if (fold && nchunks >= 4) {
+            do_chunk(0, IC<0>{});
+            do_chunk(1, IC<1>{});
+            do_chunk(2, IC<2>{});
+            do_chunk(3, IC<3>{});
+            chunk0 = 4;
         }
     }
+    for (int chunk = chunk0; chunk < nchunks; ++chunk) do_chunk(chunk, IC<-1>{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier(); // all waves done reading the ring before it becomes the epilogue image
     conv_stamp(2, srow);

@@ -388,6 +388,71 @@ __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src&
                                                                       with_bias, bslot);
 }
 
+// A refill whose LDS-DMA pieces are issued one per MFMA of the next step instead of in one block
+// before the MFMAs (a block of 7-11 LDS-DMA issues per wave ran ~1,000-2,600 cycles with the
+// matrix pipe idle: tools/trunk_items.py "reads+refill").  Same pieces, same count, same slots.
+struct Refill {
+    bool on;
+    Src src;
+    uint32_t so, wo;   // halo source offset of the chunk, weight offset
+    char* dst;         // slot base in LDS
+    bool bias;
+    int bslot;
+};
+
+// Piece p of this wave's share (p < HPW: halo, then weights, then the bias); p is a constant
+// once the MFMA loop it is called from is unrolled.
+template <int WM, int HPW, int WPW, int BIASB>
+__device__ __forceinline__ uint32_t refill_piece_k(const uint32_t* hoff, int abl, const Refill& rf, const int p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    if (p < HPW) {
+        const int j = wave + WM * p;
+        if (!(abl & 1) && j < tk::HP) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.x), ISR_LDS_PTR(rf.dst + j * 1024), 16, hoff[p],
+                                                     rf.so, 0, 16);
+            return 1;
+        }
+        return 0;
+    }
+    if (p < HPW + WPW) {
+        const int j = wave + WM * (p - HPW);
+        if (j < rf.src.wpc) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.w), ISR_LDS_PTR(rf.dst + (tk::HP + j) * 1024), 16,
+                                                     lane * 16, rf.wo + j * 1024, 0, 0);
+            return 1;
+        }
+        return 0;
+    }
+    if (p == HPW + WPW && rf.bias && wave == 0) {
+        if (lane < (rf.src.wpc == tk::WPG ? 32 : 64))  // cout floats only
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.b), ISR_LDS_PTR(smem + BIASB + rf.bslot * 256), 4,
+                                                     lane * 4, 0, 0, 0);
+        return 1;
+    }
+    return 0;
+}
+
+template <class K>
+__device__ __forceinline__ uint32_t refill_piece(const TrunkCtx<K>& c, const Refill& rf, const int p) {
+    return refill_piece_k<K::WM, K::HPW, K::WPW, K::BIAS_OFF>(c.hoff, c.abl, rf, p);
+}
+
+template <class K>
+__device__ __forceinline__ Refill make_refill(const TrunkCtx<K>& c, const Src& s, int chunk, int slot, bool with_bias,
+                                              int bslot) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    Refill rf;
+    rf.on = true;
+    rf.src = s;
+    rf.so = s.h0 + (uint32_t)chunk * c.pstride;
+    rf.wo = (uint32_t)(chunk * s.wpc * 1024);
+    rf.dst = smem + slot * K::SLOT;
+    rf.bias = with_bias;
+    rf.bslot = bslot;
+    return rf;
+}
+
 // s_waitcnt vmcnt(n) for a run-time n (0..63): this wave's n youngest vector-memory
 // instructions may stay in flight.
 __device__ __forceinline__ void wait_vm(uint32_t n) {
@@ -408,6 +473,8 @@ __device__ __forceinline__ void wait_vm(uint32_t n) {
     }
 #undef ISR_VMW
 }
+
+template <int V> struct TIC { static constexpr int value = V; };
 
 // A operand of the residual fold: (1/s1) I on couts [16 h16, 16 h16 + 16) of a 32-cout
 // fragment (lane l supplies A[l & 31][8 (l >> 5) .. + 8]); conv3x3.hip builds the same.
@@ -518,135 +585,186 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
 
     f32x16 acc[R][NF];
 
-    for (int ch = 0; ch < nch; ++ch, ++st.item) {
-        const int slot = st.item % NST;
-        const bool stamp_tile = t == (int)blockIdx.x;
-        item_stamp(L, stamp_tile, ch, 0, K::WM);
-        // ---- top of item: this item's DMA has landed for every wave ----
-        if (st.staged < st.item) {
-            // not staged (the next tile needed this tile's own outputs): drain, publish, wait, stage
-            force_publish(c, st);
-            if (ch >= first_new && !dep_ok) {
-                wait_deps(t, need);
-                dep_ok = true;
-            }
-            st.issued += stage_chunk(c, me, ch, slot, ch == 0, bslot);
-            st.staged = st.item;
-            push_mark(st);
-        }
-        wait_vm(st.issued - st.m0);
-        item_stamp(L, stamp_tile, ch, 1, K::WM);
-        raw_barrier();
-        item_stamp(L, stamp_tile, ch, 2, K::WM);
-        if (st.pend_t >= 0 && (int)(st.m0 - st.pend_mark) >= 0) {  // its stores are older than this DMA
-            if (threadIdx.x == 0)
-                __hip_atomic_store(c.state + 4 + st.pend_t, st.pend_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            st.pend_t = -1;
-        }
-        if (ch == 0) {
-            trunk_stamp(L, t, c.ntiles, 1);
-            // bias → accumulators (register g of lane l: cout (g&3) + 8(g>>2) + 4hh of fragment f)
-            const float* bs = reinterpret_cast<const float*>(smem + K::BIAS_OFF + bslot * 256);
-#pragma unroll
-            for (int f = 0; f < NF; ++f) {
-                f32x16 b0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const f32x4 q = *reinterpret_cast<const f32x4*>(bs + f * 32 + 8 * j + 4 * hh);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) b0[4 * j + e] = q[e];
-                }
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r][f] = b0;
-            }
-        }
-        const char* sb = smem + slot * K::SLOT;
-        bf16x8 fb[2][TN][NF], fa[2][NA];
-        auto read_one = [&](int dx, int idx, int set) {
-            if (idx < TN * NF) {
-                const int dyi = idx / NF, f = idx % NF;
-                fb[set][dyi][f] = lds_read16(sb + a_w + ((dyi * 3 + dx) * CT * 2 + f * 64) * 16);
-            } else {
-                const int ia = idx - TN * NF;
-                fa[set][ia] = lds_read16(sb + a_h[dx] + ia * tk::HC * 32);
-            }
-        };
-        auto read_fb = [&](int dx, int dyi, int set) {
-#pragma unroll
-            for (int f = 0; f < NF; ++f) read_one(dx, dyi * NF + f, set);
-        };
-        // step 0's fragments in order of first use (kernel-row-major MFMA order below)
-        read_fb(0, 0, 0);
-#pragma unroll
-        for (int ia = 0; ia < R; ++ia) read_one(0, TN * NF + ia, 0);
-        read_fb(0, 1, 0);
-        read_one(0, TN * NF + R, 0);
-        read_fb(0, 2, 0);
-        read_one(0, TN * NF + R + 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-
-        // ---- refill: stage the stream up to NST-1 items ahead (own chunks, then the next tile's) ----
-        while (st.staged < st.item + NST - 1) {
-            const int off = st.staged + 1 - first_item;  // chunk offset from this tile's chunk 0
-            const int nslot = (st.staged + 1) % NST;
-            if (off < nch) {
-                if (off >= first_new && !dep_ok) {
+    // one K-chunk; FC = the chunk index (0..3) when the residual fold adds its MFMAs to it, else -1
+    // (peeled so that the fold's target accumulator is compile-time: a run-time choice made hipcc
+    // MFMA into a temporary and copy 16 VGPRs back)
+    const uint32_t idv = rec_idv(rec);
+    auto do_chunk = [&](const int ch, auto fc_tag) {
+        constexpr int FC = decltype(fc_tag)::value;
+            const int slot = st.item % NST;
+            const bool stamp_tile = t == (int)blockIdx.x;
+            item_stamp(L, stamp_tile, ch, 0, K::WM);
+            // ---- top of item: this item's DMA has landed for every wave ----
+            if (st.staged < st.item) {
+                // not staged (the next tile needed this tile's own outputs): drain, publish, wait, stage
+                force_publish(c, st);
+                if (ch >= first_new && !dep_ok) {
                     wait_deps(t, need);
                     dep_ok = true;
                 }
-                st.issued += stage_chunk(c, me, off, nslot, false, 0);
-            } else {
-                const int nc = off - nch;
-                if (!nx.exists || nc >= nx.nch) break;
-                if (nx.L > 0 && nc >= nx.first_new && !st.dep_next) {
-                    if (nx.self_dep) break;  // needs this tile's outputs: staged at its own top
-                    wait_deps(nx.t, c.gen * 1024u + (unsigned)nx.L);
-                    st.dep_next = true;
-                }
-                st.issued += stage_chunk(c, nx.src, nc, nslot, nc == 0, (bslot + 1) & 3);
+                st.issued += stage_chunk(c, me, ch, slot, ch == 0, bslot);
+                st.staged = st.item;
+                push_mark(st);
             }
-            ++st.staged;
-            push_mark(st);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        item_stamp(L, stamp_tile, ch, 3, K::WM);
-
-        // ---- MFMAs: 3 steps (dx), each in kernel-row-major order (dy, then output row r):
-        // every accumulator still sees dy 0, 1, 2 in that order (conv3x3.hip's input-row-major
-        // loop gives each accumulator the same sequence, so the bits agree).  The next step's
-        // fragment of kernel row dy is read right after that row's last MFMA here, and its
-        // input row ia right after the current one's last use. ----
-#pragma unroll
-        for (int stp = 0; stp < 3; ++stp) {
-            const int cur = stp & 1;
-#pragma unroll
-            for (int dyi = 0; dyi < TN; ++dyi) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-#pragma unroll
-                    for (int f = 0; f < NF; ++f) acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][r + dyi], acc[r][f]);
-                    if constexpr (NF == 2) {
-                        // residual fold: + x/s1 on the centre pixels of row r (dx = 1, dy = 1),
-                        // between the row's dy = 1 and dy = 2 contributions
-                        if (dyi == 1 && stp == 1 && fold && ch < 4) {
-                            const bf16x8 a = fold_a_bits(rec_idv(rec), ch & 1);
-                            if (ch < 2) acc[r][0] = mfma32(a, fa[cur][r + 1], acc[r][0]);
-                            else acc[r][1] = mfma32(a, fa[cur][r + 1], acc[r][1]);
-                        }
+            wait_vm(st.issued - st.m0);
+            item_stamp(L, stamp_tile, ch, 1, K::WM);
+            raw_barrier();
+            item_stamp(L, stamp_tile, ch, 2, K::WM);
+            if (st.pend_t >= 0 && (int)(st.m0 - st.pend_mark) >= 0) {  // its stores are older than this DMA
+                if (threadIdx.x == 0)
+                    __hip_atomic_store(c.state + 4 + st.pend_t, st.pend_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                st.pend_t = -1;
+            }
+            if (ch == 0) {
+                trunk_stamp(L, t, c.ntiles, 1);
+                // bias → accumulators (register g of lane l: cout (g&3) + 8(g>>2) + 4hh of fragment f)
+                const float* bs = reinterpret_cast<const float*>(smem + K::BIAS_OFF + bslot * 256);
+    #pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    f32x16 b0;
+    #pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const f32x4 q = *reinterpret_cast<const f32x4*>(bs + f * 32 + 8 * j + 4 * hh);
+    #pragma unroll
+                        for (int e = 0; e < 4; ++e) b0[4 * j + e] = q[e];
                     }
-                    // input row ia = r + dyi is last used here when dyi == min(2, ia)
-                    if (stp + 1 < 3 && (dyi == 2 || r == 0)) read_one(stp + 1, TN * NF + r + dyi, cur ^ 1);
-                    __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                    for (int r = 0; r < R; ++r) acc[r][f] = b0;
                 }
-                if (stp + 1 < 3) {
-                    read_fb(stp + 1, dyi, cur ^ 1);
+            }
+            const char* sb = smem + slot * K::SLOT;
+            bf16x8 fb[2][TN][NF], fa[2][NA];
+            auto read_one = [&](int dx, int idx, int set) {
+                if (idx < TN * NF) {
+                    const int dyi = idx / NF, f = idx % NF;
+                    fb[set][dyi][f] = lds_read16(sb + a_w + ((dyi * 3 + dx) * CT * 2 + f * 64) * 16);
+                } else {
+                    const int ia = idx - TN * NF;
+                    fa[set][ia] = lds_read16(sb + a_h[dx] + ia * tk::HC * 32);
+                }
+            };
+            auto read_fb = [&](int dx, int dyi, int set) {
+    #pragma unroll
+                for (int f = 0; f < NF; ++f) read_one(dx, dyi * NF + f, set);
+            };
+            // step 0's fragments in order of first use (kernel-row-major MFMA order below)
+            read_fb(0, 0, 0);
+    #pragma unroll
+            for (int ia = 0; ia < R; ++ia) read_one(0, TN * NF + ia, 0);
+            read_fb(0, 1, 0);
+            read_one(0, TN * NF + R, 0);
+            read_fb(0, 2, 0);
+            read_one(0, TN * NF + R + 1, 0);
+            __builtin_amdgcn_sched_barrier(0);
+
+            // ---- refill: stage the stream up to NST-1 items ahead (own chunks, then the next tile's).
+            // The last item to stage is deferred: its pieces go out one per MFMA of step 0 below
+            // (an earlier one in the same pass is issued at once, when a later one follows). ----
+            Refill rf;
+            rf.on = false;
+            while (st.staged < st.item + NST - 1) {
+                const int off = st.staged + 1 - first_item;  // chunk offset from this tile's chunk 0
+                const int nslot = (st.staged + 1) % NST;
+                Refill nrf;
+                if (off < nch) {
+                    if (off >= first_new && !dep_ok) {
+                        if (rf.on) {  // a blocking wait publishes first: issue what is pending
+                            st.issued += stage_chunk(c, rf.src, (int)((rf.so - rf.src.h0) / c.pstride),
+                                                     (int)((rf.dst - smem) / K::SLOT), rf.bias, rf.bslot);
+                            push_mark(st);
+                            rf.on = false;
+                        }
+                        wait_deps(t, need);
+                        dep_ok = true;
+                    }
+                    nrf = make_refill(c, me, off, nslot, false, 0);
+                } else {
+                    const int nc = off - nch;
+                    if (!nx.exists || nc >= nx.nch) break;
+                    if (nx.L > 0 && nc >= nx.first_new && !st.dep_next) {
+                        if (nx.self_dep) break;  // needs this tile's outputs: staged at its own top
+                        if (rf.on) {
+                            st.issued += stage_chunk(c, rf.src, (int)((rf.so - rf.src.h0) / c.pstride),
+                                                     (int)((rf.dst - smem) / K::SLOT), rf.bias, rf.bslot);
+                            push_mark(st);
+                            rf.on = false;
+                        }
+                        wait_deps(nx.t, c.gen * 1024u + (unsigned)nx.L);
+                        st.dep_next = true;
+                    }
+                    nrf = make_refill(c, nx.src, nc, nslot, nc == 0, (bslot + 1) & 3);
+                }
+                if (rf.on) {  // an earlier deferred item: issue it now (its mark precedes this one's)
+                    st.issued += stage_chunk(c, rf.src, (int)((rf.so - rf.src.h0) / c.pstride),
+                                             (int)((rf.dst - smem) / K::SLOT), rf.bias, rf.bslot);
+                    push_mark(st);
+                }
+                rf = nrf;
+                ++st.staged;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            item_stamp(L, stamp_tile, ch, 3, K::WM);
+            uint32_t rf_n = 0;
+
+            // ---- MFMAs: 3 steps (dx), each in kernel-row-major order (dy, then output row r):
+            // every accumulator still sees dy 0, 1, 2 in that order (conv3x3.hip's input-row-major
+            // loop gives each accumulator the same sequence, so the bits agree).  The next step's
+            // fragment of kernel row dy is read right after that row's last MFMA here, and its
+            // input row ia right after the current one's last use. ----
+    #pragma unroll
+            for (int stp = 0; stp < 3; ++stp) {
+                const int cur = stp & 1;
+    #pragma unroll
+                for (int dyi = 0; dyi < TN; ++dyi) {
+    #pragma unroll
+                    for (int r = 0; r < R; ++r) {
+    #pragma unroll
+                        for (int f = 0; f < NF; ++f) acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][r + dyi], acc[r][f]);
+                        if constexpr (NF == 2 && FC >= 0) {
+                            // residual fold: + x/s1 on the centre pixels of row r (dx = 1, dy = 1),
+                            // between the row's dy = 1 and dy = 2 contributions (chunk FC, compile-time)
+                            if (dyi == 1 && stp == 1) {
+                                const bf16x8 a = fold_a_bits(idv, FC & 1);
+                                acc[r][FC >> 1] = mfma32(a, fa[cur][r + 1], acc[r][FC >> 1]);
+                            }
+                        }
+                        // input row ia = r + dyi is last used here when dyi == min(2, ia)
+                        if (stp + 1 < 3 && (dyi == 2 || r == 0)) read_one(stp + 1, TN * NF + r + dyi, cur ^ 1);
+                        if (stp == 0 && rf.on) rf_n += refill_piece<K>(c, rf, dyi * R + r);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    if (stp + 1 < 3) {
+                        read_fb(stp + 1, dyi, cur ^ 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+                if (stp == 0 && rf.on) {
+                    // pieces beyond step 0's MFMA count (the 8-wave form), then the item's mark
+    #pragma unroll
+                    for (int q = TN * R; q <= K::HPW + K::WPW; ++q) rf_n += refill_piece<K>(c, rf, q);
+                    st.issued += rf_n;
+                    push_mark(st);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+            item_stamp(L, stamp_tile, ch, 4, K::WM);
+            pop_mark(st);  // the FIFO head moves to the next item (marks are positions from st.item)
+    };
+    int ch0 = 0;
+    if constexpr (NF == 2) {
+        if (fold && nch >= 4) {
+            do_chunk(0, TIC<0>{});
+            ++st.item;
+            do_chunk(1, TIC<1>{});
+            ++st.item;
+            do_chunk(2, TIC<2>{});
+            ++st.item;
+            do_chunk(3, TIC<3>{});
+            ++st.item;
+            ch0 = 4;
         }
-        item_stamp(L, stamp_tile, ch, 4, K::WM);
-        pop_mark(st);  // the FIFO head moves to the next item (marks are positions from st.item)
     }
+    for (int ch = ch0; ch < nch; ++ch, ++st.item) do_chunk(ch, TIC<-1>{});
     trunk_stamp(L, t, c.ntiles, 2);
 
     // the neighbourhood must be done with layer L-1 before this tile's outputs land (a layer
