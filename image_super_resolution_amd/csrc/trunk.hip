@@ -388,6 +388,15 @@ __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src&
                                                                       with_bias, bslot);
 }
 
+// Interleaved refill (pieces one per step-0 MFMA): OFF in production (-DISR_TRUNK_INTERLEAVE=1 to
+// build it).  Its first GPU run, together with a rewrite of the refill loop that broke the 8-wave
+// form (wrong outputs), faulted the card in tests/test_gpu_chain.py at 16 x 128²; the loop is
+// back to its tested form and the deferral now only takes the last item of a pass.
+#ifndef ISR_TRUNK_INTERLEAVE
+#define ISR_TRUNK_INTERLEAVE 0
+#endif
+constexpr bool kTrunkInterleave = ISR_TRUNK_INTERLEAVE != 0;
+
 // A refill whose LDS-DMA pieces are issued one per MFMA of the next step instead of in one block
 // before the MFMAs (a block of 7-11 LDS-DMA issues per wave ran ~1,000-2,600 cycles with the
 // matrix pipe idle: tools/trunk_items.py "reads+refill").  Same pieces, same count, same slots.
@@ -665,42 +674,38 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
             while (st.staged < st.item + NST - 1) {
                 const int off = st.staged + 1 - first_item;  // chunk offset from this tile's chunk 0
                 const int nslot = (st.staged + 1) % NST;
-                Refill nrf;
                 if (off < nch) {
                     if (off >= first_new && !dep_ok) {
-                        if (rf.on) {  // a blocking wait publishes first: issue what is pending
-                            st.issued += stage_chunk(c, rf.src, (int)((rf.so - rf.src.h0) / c.pstride),
-                                                     (int)((rf.dst - smem) / K::SLOT), rf.bias, rf.bslot);
-                            push_mark(st);
-                            rf.on = false;
-                        }
                         wait_deps(t, need);
                         dep_ok = true;
                     }
-                    nrf = make_refill(c, me, off, nslot, false, 0);
+                    if constexpr (kTrunkInterleave) {
+                        if (st.staged + 1 == st.item + NST - 1) {  // the last item of this pass: deferred
+                            rf = make_refill(c, me, off, nslot, false, 0);
+                            ++st.staged;
+                            break;
+                        }
+                    }
+                    st.issued += stage_chunk(c, me, off, nslot, false, 0);
                 } else {
                     const int nc = off - nch;
                     if (!nx.exists || nc >= nx.nch) break;
                     if (nx.L > 0 && nc >= nx.first_new && !st.dep_next) {
                         if (nx.self_dep) break;  // needs this tile's outputs: staged at its own top
-                        if (rf.on) {
-                            st.issued += stage_chunk(c, rf.src, (int)((rf.so - rf.src.h0) / c.pstride),
-                                                     (int)((rf.dst - smem) / K::SLOT), rf.bias, rf.bslot);
-                            push_mark(st);
-                            rf.on = false;
-                        }
                         wait_deps(nx.t, c.gen * 1024u + (unsigned)nx.L);
                         st.dep_next = true;
                     }
-                    nrf = make_refill(c, nx.src, nc, nslot, nc == 0, (bslot + 1) & 3);
+                    if constexpr (kTrunkInterleave) {
+                        if (st.staged + 1 == st.item + NST - 1) {
+                            rf = make_refill(c, nx.src, nc, nslot, nc == 0, (bslot + 1) & 3);
+                            ++st.staged;
+                            break;
+                        }
+                    }
+                    st.issued += stage_chunk(c, nx.src, nc, nslot, nc == 0, (bslot + 1) & 3);
                 }
-                if (rf.on) {  // an earlier deferred item: issue it now (its mark precedes this one's)
-                    st.issued += stage_chunk(c, rf.src, (int)((rf.so - rf.src.h0) / c.pstride),
-                                             (int)((rf.dst - smem) / K::SLOT), rf.bias, rf.bslot);
-                    push_mark(st);
-                }
-                rf = nrf;
                 ++st.staged;
+                push_mark(st);
             }
             __builtin_amdgcn_sched_barrier(0);
             item_stamp(L, stamp_tile, ch, 3, K::WM);

@@ -15,6 +15,8 @@ bar of test_gpu_parity.py does not apply; the full-depth tanh-space bar does):
         HBM): mean |d| <= 0.5 LSB, and at most a third of the halo-0 stitch's error
         (measured 0.24 vs 1.53 LSB);
   (iii) shard_tiles(tiles, 8) (SURVEY.md §8e LPT deal): max rank load <= 1.05 x mean;
+  (iv)  the 8-rank band deal (tiler.plan_bands, every rank's share run on this GPU and
+        stitched): vs the whole-image forward within the halo-32 bar of (ii);
   plus: the plan cache stays within its byte budget.
 """
 import os
@@ -137,3 +139,55 @@ def test_cfg4_shard_balance():
     assert sorted(t.index for s in shards for t in s) == list(range(40))
     loads = [sum(t.cost for t in s) for s in shards]
     assert max(loads) <= 1.05 * sum(loads) / 8, loads
+
+
+def _stitch(shards, done, shape):
+    canvas = torch.zeros(shape, dtype=torch.uint8, device=DEV)
+    for lst in shards:
+        for t in lst:
+            canvas[:, t.y * S:(t.y + t.h) * S, t.x * S:(t.x + t.w) * S] = done[t.index]
+    return canvas
+
+
+@torch.no_grad()
+def test_cfg4_bands_vs_whole_image(setup):
+    """Each of 8 ranks' bands (one 334- or 302-row full-width band per rank) run on this GPU,
+    stitched: the canvas rank 0 would assemble, against one whole-image forward."""
+    r = setup["runner"]
+    up = tiler.TileUpscaler(r, S, window=WINDOW, halo=HALO, batch=4, device=DEV, shard="bands")
+    img = setup["img"].to(DEV)
+    shards = up.shards(H, W, 8)
+    assert all(len({t.in_shape for t in lst}) == 1 for lst in shards)
+    done = {}
+    for lst in shards:
+        done.update(up.run_tiles(img, lst))
+        r.verify()
+    canvas = _stitch(shards, done, setup["canvas"].shape)
+    whole = setup["model"](img[None])[0]
+    err = (canvas.float() - whole.float()).abs().mean().item()
+    print(f"mean |bands - whole| (LSB): {err:.4f}")
+    assert err <= 0.5, err
+
+
+@torch.no_grad()
+def test_bands_with_full_receptive_halo_equal_whole_image_bitwise():
+    """With a halo at least the network's receptive radius (ResNet(1) x4: 9x9 head 4 + 15 RDB
+    convs + conv1 + the Scaler and 9x9 tail convs < 24 LR px) every band output pixel sees the
+    same inputs and the same arithmetic as in one whole-image forward: bit-identical canvas."""
+    net = models.ResNet(1, 0.2, scaleRate=S)
+    net.load_state_dict(synth_state_dict(net.state_dict(), seed=8))
+    m = models.Model(net)
+    m.init_normalize([0.485, 0.456, 0.406], [0.229, 0.224, 0.225])
+    m = m.eval().fuse().to(DEV)
+    g = torch.Generator().manual_seed(3)
+    img = torch.randint(0, 256, (3, 150, 230), generator=g, dtype=torch.uint8).to(DEV)
+    runner = tiler.runner_for(m, DEV)
+    whole = m(img[None])[0]
+    up = tiler.TileUpscaler(runner, S, window=64, halo=24, batch=2, device=DEV, shard="bands")
+    for world in (2, 3):
+        shards = up.shards(150, 230, world)
+        done = {}
+        for lst in shards:
+            done.update(up.run_tiles(img, lst))
+        runner.verify()
+        assert torch.equal(_stitch(shards, done, whole.shape), whole), world
