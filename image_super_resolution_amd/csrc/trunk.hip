@@ -679,7 +679,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                         wait_deps(t, need);
                         dep_ok = true;
                     }
-                    if constexpr (kTrunkInterleave) {
+                    if constexpr (kTrunkInterleave && NST == 2) {
                         if (st.staged + 1 == st.item + NST - 1) {  // the last item of this pass: deferred
                             rf = make_refill(c, me, off, nslot, false, 0);
                             ++st.staged;
@@ -695,7 +695,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                         wait_deps(nx.t, c.gen * 1024u + (unsigned)nx.L);
                         st.dep_next = true;
                     }
-                    if constexpr (kTrunkInterleave) {
+                    if constexpr (kTrunkInterleave && NST == 2) {
                         if (st.staged + 1 == st.item + NST - 1) {
                             rf = make_refill(c, nx.src, nc, nslot, nc == 0, (bslot + 1) & 3);
                             ++st.staged;

@@ -125,7 +125,9 @@ class GeneratorTrainPlan:
         # ---- activations (saved for the backward)
         self.f0 = ActBuffer.alloc(n, h, w, 64, 1, dev)
         nr = len(self.rdbs)
-        self.D = [ActBuffer.alloc(n, h, w, 192, 1, dev) for _ in range(nr)] + [ActBuffer.alloc(n, h, w, 64, 1, dev)]
+        # the trunk output buffer carries 192 channels too (only [0, 64) is used): the persistent
+        # trunk kernel needs every layer's views in one buffer geometry (trunk.hip records)
+        self.D = [ActBuffer.alloc(n, h, w, 192, 1, dev) for _ in range(nr + 1)]
         self.T = ActBuffer.alloc(n, h, w, 64, 1, dev)
         self.ups = []
         hh, ww, ha, wa = h, w, self.f0.ha, self.f0.wa
@@ -264,7 +266,9 @@ class GeneratorTrainPlan:
             try:
                 from .engine import CHAIN_ACQUIRE
                 self.chain = ConvChain([e[1] for e in F[trunk0:]], D[0], self.device, acquire=CHAIN_ACQUIRE)
-            except ValueError:
+            except ValueError as e:  # not silent: the per-conv trunk costs ~3.5 ms per SRGAN step
+                import warnings
+                warnings.warn(f"training trunk runs per conv (persistent trunk kernel refused the layers: {e})")
                 self.chain = None
             if self.chain is not None:
                 F[trunk0:] = [(self.chain.fn, self.chain.desc)]
