@@ -388,14 +388,20 @@ __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src&
                                                                       with_bias, bslot);
 }
 
-// Interleaved refill (pieces one per step-0 MFMA): OFF in production (-DISR_TRUNK_INTERLEAVE=1 to
-// build it).  Its first GPU run, together with a rewrite of the refill loop that broke the 8-wave
-// form (wrong outputs), faulted the card in tests/test_gpu_chain.py at 16 x 128²; the loop is
-// back to its tested form and the deferral now only takes the last item of a pass.
+// Interleaved refill (the pair form's one refill item issued one piece per MFMA of step 0 or, with
+// -DISR_TRUNK_INTERLEAVE=2, of step 2): OFF.  Bit-identical (tests/test_gpu_chain.py) but slower:
+// 7.41 / 7.47 ms per bench forward against 6.64 ms for the block issue, same box, two rounds each
+// (profiles/r03_trunk_interleave_ab.jsonl) — the LDS-DMA issue stalls the wave's in-order MFMA
+// stream wherever it sits, so spreading it only adds the stalls to the matrix-pipe chain.  (A
+// first version also rewrote the refill loop; that rewrite broke the 8-wave form and faulted the
+// card once — the loop is back to its tested form.)
 #ifndef ISR_TRUNK_INTERLEAVE
 #define ISR_TRUNK_INTERLEAVE 0
 #endif
 constexpr bool kTrunkInterleave = ISR_TRUNK_INTERLEAVE != 0;
+// the step (dx) whose MFMAs carry the pieces: 0 (interleave 1) or 2 (interleave 2: after the
+// chunk's last LDS fragment read, so no later read of this chunk can be held behind the DMA)
+constexpr int kTrunkInterleaveStep = ISR_TRUNK_INTERLEAVE == 2 ? 2 : 0;
 
 // A refill whose LDS-DMA pieces are issued one per MFMA of the next step instead of in one block
 // before the MFMAs (a block of 7-11 LDS-DMA issues per wave ran ~1,000-2,600 cycles with the
@@ -735,7 +741,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                         }
                         // input row ia = r + dyi is last used here when dyi == min(2, ia)
                         if (stp + 1 < 3 && (dyi == 2 || r == 0)) read_one(stp + 1, TN * NF + r + dyi, cur ^ 1);
-                        if (stp == 0 && rf.on) rf_n += refill_piece<K>(c, rf, dyi * R + r);
+                        if (stp == kTrunkInterleaveStep && rf.on) rf_n += refill_piece<K>(c, rf, dyi * R + r);
                         __builtin_amdgcn_sched_barrier(0);
                     }
                     if (stp + 1 < 3) {
@@ -743,7 +749,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 }
-                if (stp == 0 && rf.on) {
+                if (stp == kTrunkInterleaveStep && rf.on) {
                     // pieces beyond step 0's MFMA count (the 8-wave form), then the item's mark
     #pragma unroll
                     for (int q = TN * R; q <= K::HPW + K::WPW; ++q) rf_n += refill_piece<K>(c, rf, q);
