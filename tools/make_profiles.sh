@@ -19,12 +19,12 @@ cp $T/prof_bench/bench_kernel_stats.csv $P/${R}_bench_kernel_stats.csv
 python3 - "$T/prof_bench/bench_kernel_trace.csv" "$P/${R}_bench_dominant_by_grid.json" <<'EOF2'
 import csv, json, sys
 from collections import defaultdict
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "conv_chain_kernel" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "trunk_kernel" in r["Kernel_Name"]]
 by = defaultdict(list)
 for r in rows:
     by[int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 out = [{"kernel": rows[0]["Kernel_Name"], "blocks": b, "dispatches": len(v), "avg_us": round(sum(v) / len(v) / 1e3, 3),
-        "role": "persistent trunk kernel, one launch per forward"}
+        "role": "persistent trunk kernel (trunk.hip), one launch per forward"}
        for b, v in sorted(by.items())]
 json.dump(out, open(sys.argv[2], "w"), indent=1)
 print(json.dumps(out))
@@ -37,14 +37,14 @@ R, P = sys.argv[1], sys.argv[2]
 rows = json.load(open(f"{P}/{R}_pmc_summary.json"))
 # kernel families bench.py reports a roofline for (bench.py load_traffic): the persistent
 # trunk kernel, the per-conv growth (V_G0) and final (V_F0) templates, the 9x9 tail
-fam = {"chain": "conv_chain_kernel", "growth": "C3<4, 4, 1, 16, 2, 0, 0, 2",
+fam = {"chain": "trunk_kernel<", "growth": "C3<4, 4, 1, 16, 2, 0, 0, 2",
        "final": "C3<4, 4, 2, 16, 2, 192", "tail": "tail9x9_"}
 out = {"families": {},
        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, KiB -> bytes, FETCH_SIZE x2 "
                  "(gfx950 wide-load correction, MI355X_MICROARCH.md §HBM); mean over dispatches of the "
                  "largest grid of the family; Infinity-Cache hits are included in these counters"}
 for k, sub in fam.items():
-    dom = [r for r in rows if sub in r["kernel"] and (k != "growth" or "conv_chain" not in r["kernel"])]
+    dom = [r for r in rows if sub in r["kernel"] and (k != "growth" or "chain" not in r["kernel"])]
     if not dom:
         continue
     g = max(int(r["grid"]) for r in dom)
