@@ -395,6 +395,9 @@ __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src&
 // stream wherever it sits, so spreading it only adds the stalls to the matrix-pipe chain.  (A
 // first version also rewrote the refill loop; that rewrite broke the 8-wave form and faulted the
 // card once — the loop is back to its tested form.)
+#ifndef ISR_TRUNK_PRIO
+#define ISR_TRUNK_PRIO 0  // tuning builds of an A/B only (1: per-chunk MFMA priority, 2: static)
+#endif
 #ifndef ISR_TRUNK_INTERLEAVE
 #define ISR_TRUNK_INTERLEAVE 0
 #endif
@@ -716,6 +719,9 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
             __builtin_amdgcn_sched_barrier(0);
             item_stamp(L, stamp_tile, ch, 3, K::WM);
             uint32_t rf_n = 0;
+#if ISR_TRUNK_PRIO == 1
+            __builtin_amdgcn_s_setprio(1);  // tuning A/B: MFMA stream ahead of the partner's issue
+#endif
 
             // ---- MFMAs: 3 steps (dx), each in kernel-row-major order (dy, then output row r):
             // every accumulator still sees dy 0, 1, 2 in that order (conv3x3.hip's input-row-major
@@ -758,6 +764,9 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+#if ISR_TRUNK_PRIO == 1
+            __builtin_amdgcn_s_setprio(0);
+#endif
             item_stamp(L, stamp_tile, ch, 4, K::WM);
             pop_mark(st);  // the FIFO head moves to the next item (marks are positions from st.item)
     };
@@ -894,6 +903,10 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
         for (int k = 0; k < K::HPW; ++k) c.hoff[k] = halo_piece_off(wave + K::WM * k, lane, c.wp);
     }
     const int G = gridDim.x, b = blockIdx.x;
+#if ISR_TRUNK_PRIO == 2
+    // tuning A/B: the later-dispatched half of the grid (a CU's second workgroup) at priority 1
+    if (__builtin_amdgcn_readfirstlane(b) >= G / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     Stream<K> st;
     st.item = 0;
     st.staged = 0;
