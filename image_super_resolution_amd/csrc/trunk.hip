@@ -395,8 +395,13 @@ __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src&
 // stream wherever it sits, so spreading it only adds the stalls to the matrix-pipe chain.  (A
 // first version also rewrote the refill loop; that rewrite broke the 8-wave form and faulted the
 // card once — the loop is back to its tested form.)
+// Wave priority: 1 (production) raises the wave to priority 1 around each chunk's MFMA stream
+// (s_setprio, cdna_hip_programming.md T5), so the co-resident workgroup's refill / epilogue issue
+// yields to it: 6.567 / 6.566 vs 6.620 / 6.592 ms per bench forward, same box, two rounds
+// (profiles/r03_trunk_prio_ab.jsonl); 2 (a static priority for the later-dispatched half of the
+// grid) measured no change; 0 = none.
 #ifndef ISR_TRUNK_PRIO
-#define ISR_TRUNK_PRIO 0  // tuning builds of an A/B only (1: per-chunk MFMA priority, 2: static)
+#define ISR_TRUNK_PRIO 1
 #endif
 #ifndef ISR_TRUNK_INTERLEAVE
 #define ISR_TRUNK_INTERLEAVE 0
@@ -720,7 +725,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
             item_stamp(L, stamp_tile, ch, 3, K::WM);
             uint32_t rf_n = 0;
 #if ISR_TRUNK_PRIO == 1
-            __builtin_amdgcn_s_setprio(1);  // tuning A/B: MFMA stream ahead of the partner's issue
+            __builtin_amdgcn_s_setprio(1);  // the MFMA stream ahead of the partner's issue
 #endif
 
             // ---- MFMAs: 3 steps (dx), each in kernel-row-major order (dy, then output row r):

@@ -11,3 +11,5 @@ for r in 1 2; do
   step 120 abp_p1_$r env ISR_LIB=$PWD/ab/libisr_p1.so python -u tools/ab_chain.py --configs 1:1:0:0 --rounds 5 &&
   step 120 abp_p2_$r env ISR_LIB=$PWD/ab/libisr_p2.so python -u tools/ab_chain.py --configs 1:1:0:0 --rounds 5 || exit 1
 done
+step 300 video python -u tools/bench_video.py --frames 48
+step 200 smoke python -u -c "import __graft_entry__ as g; g.smoke()"
