@@ -215,11 +215,12 @@ class TileUpscaler:
 
     def __init__(self, runner: BatchRunner, scale: int, window: int = 96, halo: int = 0, batch: int = 8,
                  device="cuda", shard: str = "windows"):
-        """`shard` (world > 1 only): "windows" deals rs.py's windows longest-processing-time-first
-        (shard_tiles; the canvas equals the single-rank one bit for bit); "bands" gives every rank
-        full-width horizontal bands with the same halo (plan_bands; <= 2 plan shapes per rank, one
-        forward per band; needs halo > 0 to hide its seams, and differs from the windowed canvas
-        by the seams each form leaves)."""
+        """`shard`: "windows" runs rs.py's windows (dealt longest-processing-time-first over
+        ranks, shard_tiles; the canvas equals the single-rank one bit for bit); "bands" runs
+        full-width horizontal bands with the same halo (plan_bands: one rank's share is one or a
+        few bands of at most two shapes, one forward each; on one GPU the image splits into as
+        few bands as the trunk kernel's 2 GiB buffer window allows; needs halo > 0 to hide its
+        seams, and differs from the windowed canvas by the seams each form leaves)."""
         if batch < 1:
             raise ValueError("batch must be >= 1")
         if shard not in ("windows", "bands"):
@@ -230,7 +231,7 @@ class TileUpscaler:
 
     def shards(self, height: int, width: int, world: int) -> list[list[Tile]]:
         """The per-rank tile lists of an image (deterministic: every rank computes the same)."""
-        if world > 1 and self.shard == "bands":
+        if self.shard == "bands":
             return plan_bands(height, width, world, self.halo)
         tiles = plan_tiles(height, width, self.window, self.halo)
         return shard_tiles(tiles, world) if world > 1 else [tiles]
@@ -243,9 +244,11 @@ class TileUpscaler:
         for t in tiles:
             groups[t.in_shape].append(t)
         out: dict[int, torch.Tensor] = {}
+        # bands are sized to the trunk kernel's 2 GiB buffer window one at a time: batch 1
+        step = 1 if self.shard == "bands" else self.batch
         for (h, w), lst in groups.items():
-            for i in range(0, len(lst), self.batch):
-                chunk = lst[i:i + self.batch]
+            for i in range(0, len(lst), step):
+                chunk = lst[i:i + step]
                 x = torch.stack([image[:, t.y0:t.y1, t.x0:t.x1] for t in chunk])
                 y = self.runner(x)
                 if tuple(y.shape) != (len(chunk), 3, h * s, w * s):

@@ -9,11 +9,13 @@ collective), rank 0 receives finished tiles point-to-point and owns the canvas.
 Reports HR megapixels/s of the whole image (after one warm-up call that builds
 the plans), seconds per image, and peak device memory.
 
+--shard bands runs full-width bands (tiler.plan_bands) instead of rs.py's windows, on one GPU
+too (as few bands as the 2 GiB trunk-buffer window allows).
 --sim-world N (one GPU, no torch.distributed): predicts the N-GPU wall time.  After the
-1-GPU windowed run (t1), every rank's share of an N-rank deal (--shard windows: the LPT deal of
-rs.py windows; bands: tiler.plan_bands) runs alone on this GPU, timed like the real run
-(same plans, median of --reps); the predicted N-GPU time is the slowest rank's, reported
-against t1 / N.  The point-to-point gather of finished tiles to rank 0 is not included.
+1-GPU run (t1, with the same --shard), every rank's share of an N-rank deal runs alone on this
+GPU, timed like the real run (same plans, median of --reps); the predicted N-GPU time is the
+slowest rank's, reported against t1 / N.  The gather of finished tiles to rank 0 is not
+included.
 usage: python tools/bench_still.py [--reps 3] [--batch 4] [--halo 32] [--shard bands] [--sim-world 8]
 """
 from __future__ import annotations
@@ -88,11 +90,12 @@ def main():
                 el = tt.item()
             ts.append(el)
     t = statistics.median(ts)
-    tiles = tiler.plan_tiles(args.height, args.width, args.window, args.halo)
+    tiles = [tt for lst in up.shards(args.height, args.width, 1) for tt in lst]
     run_px = sum(tt.cost for tt in tiles) * 16
     res = {"metric": "cfg4 4K->16K still, HR MPix/s", "value": round(args.height * args.width * 16 / t / 1e6, 2),
            "unit": "MPix/s", "n_gpus": world, "s_per_image": round(t, 4), "s_first_call": round(warm, 3),
-           "tiles": len(tiles), "window": args.window, "halo": args.halo, "batch": args.batch,
+           "shard_1gpu": args.shard, "tiles": len(tiles), "window": args.window, "halo": args.halo,
+           "batch": args.batch,
            "shapes": sorted({tt.in_shape for tt in tiles}),
            "halo_overhead": round(run_px / (args.height * args.width * 16), 4),
            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
