@@ -103,6 +103,17 @@ def test_plan_bands_cfg4_one_plan_per_rank():
     assert 192 * 2 * (336 + 2) * (3840 + 2) < 2 ** 31
 
 
+def test_bands_single_rank_equals_whole_image():
+    """shard="bands" on one rank (as few full-width bands as the 2 GiB window allows; forced to
+    several here by a small max_rows through plan_bands' default being large): with a halo of at
+    least the operator's radius the canvas equals the whole-image run."""
+    img = image(45, 61, seed=5)
+    full = box_up(img[None])[0]
+    up = tiler.TileUpscaler(box_up, S, window=16, halo=1, batch=4, device="cpu", shard="bands")
+    assert len(up.shards(45, 61, 1)) == 1
+    assert torch.equal(up(img), full)
+
+
 def test_runner_shape_check():
     up = tiler.TileUpscaler(lambda x: x, S, window=8, device="cpu")
     with pytest.raises(RuntimeError, match="runner returned"):
