@@ -45,6 +45,12 @@ def test_train_then_upscale(tmp_path):
     rs.runer(**kw)
     out = np.asarray(Image.open(tmp_path / "out.png"))
     assert out.shape == (80, 112, 3) and out.dtype == np.uint8 and out.std() > 0
+    # --shard bands on one GPU: with a halo covering the whole 40-row image the single band is the
+    # whole-image forward, which the 64-px window run below also is
+    rs.runer(**dict(kw, save_dir=str(tmp_path / "out_bands.png"), halo=40, shard="bands"))
+    rs.runer(**dict(kw, save_dir=str(tmp_path / "out_whole.png"), window_size=64))
+    assert np.array_equal(np.asarray(Image.open(tmp_path / "out_bands.png")),
+                          np.asarray(Image.open(tmp_path / "out_whole.png")))
 
     # video: headerless rgb24 in → bgr24 out (no ffmpeg needed)
     frames = (np.random.default_rng(1).random((3, 24, 40, 3)) * 255).astype(np.uint8)
