@@ -69,11 +69,11 @@ size_t trunk_state_words(int n, int ha, int wa) {
 // err bits: 1 grid, 2 view geometry, 4 kind/cout, 8 cin/bias, 16 unsupported epilogue form,
 // 32 residual form, 64 beyond the 2 GiB buffer window, 128 too many layers.
 __global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* layers, const int32_t* kinds, int nl,
-                                                          int n, int ha, int wa, unsigned* state) {
+                                                          int n, int ha, int wa, unsigned* state, int th) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     unsigned* err = reinterpret_cast<unsigned*>(smem);
     const int L = threadIdx.x;
-    const int nbx = wa / tk::TW, nby = ha / tk::TH, ntiles = n * nbx * nby;
+    const int nbx = wa / tk::TW, nby = ha / th, ntiles = n * nbx * nby;
     const size_t ro = trunk_rec_off(ntiles);
     if (L == 0) *err = 0;
     __syncthreads();
@@ -271,15 +271,18 @@ __device__ __forceinline__ void acquire_fence() {
 // K-chunks in flight).  <4, 4, 2>: two 4-wave workgroups per CU, one chunk in flight (the
 // round-3 first form); <8, 2, 4>: one 8-wave workgroup per CU, three chunks in flight, two tiles
 // of independent images interleaved per layer.
-template <int WM_, int R_, int NST_>
+template <int WM_, int R_, int NST_, int TH_ = 16>
 struct TK {
     static constexpr int WM = WM_, R = R_, NST = NST_;
     static constexpr int NT = 64 * WM;
-    static_assert(R * WM == tk::TH, "16-row tiles");
+    static constexpr int TH = TH_;                        // tile rows (x 32 columns)
+    static constexpr int HQ = (TH + 2) * tk::HC;          // halo pixels of a chunk
+    static constexpr int HP = (HQ + 31) / 32;             // halo pieces (1 KB) per chunk
+    static_assert(R * WM == TH, "the waves cover the tile rows");
     static_assert(NST >= 2 && NST <= 4, "ring depth");
-    static constexpr int HPW = (tk::HP + WM - 1) / WM;   // halo pieces per wave (at most)
+    static constexpr int HPW = (HP + WM - 1) / WM;        // halo pieces per wave (at most)
     static constexpr int WPW = (tk::WPF + WM - 1) / WM;  // weight pieces per wave (at most)
-    static constexpr int SLOT = (tk::HP + tk::WPF) * 1024;
+    static constexpr int SLOT = (HP + tk::WPF) * 1024;
     static constexpr int BIAS_OFF = NST * SLOT;          // 4 bias slots of 256 B
     static constexpr int LDS = BIAS_OFF + 4 * 256;
     static_assert(LDS <= 163840, "LDS budget");
@@ -299,6 +302,7 @@ struct Src {
 
 template <class K>
 struct TrunkCtx {
+    static constexpr int TH = K::TH;
     unsigned* state;
     unsigned gen;
     int acquire;
@@ -313,7 +317,7 @@ __device__ __forceinline__ Src src_of(const C& c, const_rec& rec, int t) {
     const int bx = t % c.nbx, tmp = t / c.nbx, by = tmp % c.nby, img = tmp / c.nby;
     Src s;
     s.x = (const char*)(uintptr_t)rec.x;
-    s.h0 = (uint32_t)(((((uint32_t)img * c.cs16 + rec_xp(rec)) * c.hp + (by * tk::TH - 1 + c.pad)) * c.wp +
+    s.h0 = (uint32_t)(((((uint32_t)img * c.cs16 + rec_xp(rec)) * c.hp + (by * C::TH - 1 + c.pad)) * c.wp +
                        (bx * tk::TW - 1 + c.pad)) * 32);
     s.w = (const char*)(uintptr_t)rec.w;
     s.b = (const float*)(uintptr_t)rec.b;
@@ -329,10 +333,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
 // unit (q, c) sits at 2q + (c ^ bit 3 of col).  The swizzle depends on the column only, so the
 // rows a wave reads at one dx share one per-lane address (row offsets are immediates), and the
 // 16 lanes of a ds_read_b128 group (columns 8 apart pair up) still hit 16 distinct bank slots.
+template <int HQ>
 __device__ __forceinline__ uint32_t halo_piece_off(int j, int lane, int wp) {
     const int u = j * 64 + lane;
     const int q = u >> 1;
-    if (q >= tk::HQ) return 0;  // tail of the last piece: never read
+    if (q >= HQ) return 0;  // tail of the last piece: never read
     const int row = q / tk::HC, col = q - row * tk::HC;
     const int cc = (u & 1) ^ ((col >> 3) & 1);
     return (uint32_t)((row * wp + col) * 32 + cc * 16);
@@ -342,7 +347,7 @@ __device__ __forceinline__ uint32_t halo_piece_off(int j, int lane, int wp) {
 // weight pieces; wave 0 also the bias (first chunk of a tile).  Halo pieces are sc1 (L1
 // bypass: other workgroups of this launch wrote them).  Returns the vector-memory instructions
 // this wave issued (wave-uniform), for the counted waits.
-template <int WM, int HPW, int WPW, int SLOTB, int BIASB>
+template <int WM, int HPW, int WPW, int SLOTB, int BIASB, int HP>
 __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t pstride, int abl, const Src& s,
                                                   int chunk, int slot, bool with_bias, int bslot) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -355,7 +360,7 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
 #pragma unroll
         for (int k = 0; k < HPW; ++k) {
             const int j = wave + WM * k;
-            if (j < tk::HP) {
+            if (j < HP) {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, ISR_LDS_PTR(dst + j * 1024), 16, hoff[k], so, 0, 16);
                 ++n;
             }
@@ -363,7 +368,7 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
     }
     const auto rw = rsrc(s.w);
     const uint32_t wo = (uint32_t)(chunk * s.wpc * 1024);
-    char* wd = dst + tk::HP * 1024;
+    char* wd = dst + HP * 1024;
 #pragma unroll
     for (int k = 0; k < WPW; ++k) {
         const int j = wave + WM * k;
@@ -384,7 +389,7 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
 template <class K>
 __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src& s, int chunk, int slot, bool with_bias,
                                                 int bslot) {
-    return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF>(c.hoff, c.pstride, c.abl, s, chunk, slot,
+    return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF, K::HP>(c.hoff, c.pstride, c.abl, s, chunk, slot,
                                                                       with_bias, bslot);
 }
 
@@ -432,13 +437,13 @@ struct Refill {
 
 // Piece p of this wave's share (p < HPW: halo, then weights, then the bias); p is a constant
 // once the MFMA loop it is called from is unrolled.
-template <int WM, int HPW, int WPW, int BIASB>
+template <int WM, int HPW, int WPW, int BIASB, int HP>
 __device__ __forceinline__ uint32_t refill_piece_k(const uint32_t* hoff, int abl, const Refill& rf, const int p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int wave = wave_id(), lane = threadIdx.x & 63;
     if (p < HPW) {
         const int j = wave + WM * p;
-        if (!(abl & 1) && j < tk::HP) {
+        if (!(abl & 1) && j < HP) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.x), ISR_LDS_PTR(rf.dst + j * 1024), 16, hoff[p],
                                                      rf.so, 0, 16);
             return 1;
@@ -448,7 +453,7 @@ __device__ __forceinline__ uint32_t refill_piece_k(const uint32_t* hoff, int abl
     if (p < HPW + WPW) {
         const int j = wave + WM * (p - HPW);
         if (j < rf.src.wpc) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.w), ISR_LDS_PTR(rf.dst + (tk::HP + j) * 1024), 16,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.w), ISR_LDS_PTR(rf.dst + (HP + j) * 1024), 16,
                                                      lane * 16, rf.wo + j * 1024, 0, 0);
             return 1;
         }
@@ -465,7 +470,7 @@ __device__ __forceinline__ uint32_t refill_piece_k(const uint32_t* hoff, int abl
 
 template <class K>
 __device__ __forceinline__ uint32_t refill_piece(const TrunkCtx<K>& c, const Refill& rf, const int p) {
-    return refill_piece_k<K::WM, K::HPW, K::WPW, K::BIAS_OFF>(c.hoff, c.abl, rf, p);
+    return refill_piece_k<K::WM, K::HPW, K::WPW, K::BIAS_OFF, K::HP>(c.hoff, c.abl, rf, p);
 }
 
 template <class K>
@@ -584,7 +589,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     constexpr int R = K::R, NST = K::NST, CT = 32 * NF, TN = 3, NA = R + 2;
     const int wave = wave_id(), lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
     const int bx = t % c.nbx, tmp = t / c.nbx, by = tmp % c.nby, img = tmp / c.nby;
-    const int x0 = bx * tk::TW, y0 = by * tk::TH;
+    const int x0 = bx * tk::TW, y0 = by * K::TH;
     const int nch = rec_nch(rec);
     const int first_new = rec_first_new(rec);  // NEED_NONE on layer 0
     const unsigned need = c.gen * 1024u + (unsigned)L;  // the neighbourhood is done with layer L-1
@@ -598,7 +603,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     trunk_stamp(L, t, c.ntiles, 0);
 
     // per-lane LDS read addresses (slot 0): weights A[n][k] (n = cout), halo rows of this wave
-    const uint32_t a_w = (uint32_t)(tk::HP * 1024 + (2 * l31 + (hh ^ ((l31 >> 3) & 1))) * 16);
+    const uint32_t a_w = (uint32_t)(K::HP * 1024 + (2 * l31 + (hh ^ ((l31 >> 3) & 1))) * 16);
     uint32_t a_h[3];
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx)
@@ -917,7 +922,7 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
     {
         const int wave = wave_id(), lane = threadIdx.x & 63;
 #pragma unroll
-        for (int k = 0; k < K::HPW; ++k) c.hoff[k] = halo_piece_off(wave + K::WM * k, lane, c.wp);
+        for (int k = 0; k < K::HPW; ++k) c.hoff[k] = halo_piece_off<K::HQ>(wave + K::WM * k, lane, c.wp);
     }
     const int G = gridDim.x, b = blockIdx.x;
 #if ISR_TRUNK_PRIO == 2
@@ -978,8 +983,8 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
 // what the build is made for); ISR_ERR when that is below one workgroup per CU.
 template <class K>
 static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
-    if (cd->ha % tk::TH || cd->wa % tk::TW || cd->nl < 1 || cd->nl > 1024) return -2;
-    const int nbx = cd->wa / tk::TW, nby = cd->ha / tk::TH;
+    if (cd->ha % K::TH || cd->wa % tk::TW || cd->nl < 1 || cd->nl > 1024) return -2;
+    const int nbx = cd->wa / tk::TW, nby = cd->ha / K::TH;
     const long long ntiles = (long long)cd->n * nbx * nby;
     if (ntiles <= 0 || ntiles > (1 << 24)) return -2;
     static thread_local int cached_dev = -1, cached_per_cu = 0, cached_cus = 0;
@@ -1005,7 +1010,7 @@ static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
     const int grid = (int)(ntiles < slots ? ntiles : slots);
     const int rec_off = (int)trunk_rec_off((int)ntiles);
     hipLaunchKernelGGL(trunk_prep_kernel, dim3(1), dim3(1024), 16, s, cd->layers, cd->kinds, cd->nl, cd->n, cd->ha,
-                       cd->wa, cd->state);
+                       cd->wa, cd->state, K::TH);
     TrunkArgs a;
     a.state = cd->state;
     a.rec_off = rec_off;
@@ -1021,8 +1026,12 @@ static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
 // form's 2-row waves read 7 LDS fragments per 6 MFMAs (4-row waves: 9 per 12)
 using TK_PAIR = TK<4, 4, 2>;
 using TK_DEEP = TK<8, 2, 4>;   // one 8-wave workgroup per CU, 3 chunks in flight
+// 32x32 tiles: one 8-wave workgroup per CU (4 rows per wave, as the pair form), the chunk's
+// weights staged once per CU instead of twice and a (34x34)/(32x32) halo instead of (18x34)/(16x32)
+using TK_T32 = TK<8, 4, 2, 32>;
 
 int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
+    if (form == 2) return trunk_launch_k<TK_T32>(cd, s);
     return form == 1 ? trunk_launch_k<TK_DEEP>(cd, s) : trunk_launch_k<TK_PAIR>(cd, s);
 }
 

@@ -63,7 +63,8 @@ def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks):
     gw = _gw(blocks)
     xs = _inputs(n, h, w, 3, seed=3)
     refs = _run(gw, xs, chain=False)
-    for variant in (0, 2, 1):
+    # variant 3 (32x32 tiles) needs the 16-row-rounded height to be a multiple of 32
+    for variant in (0, 2, 1) + ((3,) if -(-h // 16) % 2 == 0 else ()):
         for acquire in (False, True):
             for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire, variant=variant), refs):
                 assert torch.equal(out, ref), \
