@@ -323,27 +323,32 @@ __global__ __launch_bounds__(128) void wgrad_reduce_t_kernel(WgradArgs a) {
 }
 
 // Workspace rows are [splits][9*cout*cin + cout] (the bias partials follow each
-// split's dW partials).  Block = 4 split-slices x 64 float4 columns: every
-// thread streams S/4 rows of one 16-byte column (independent loads in flight),
-// the 4 slices are summed through LDS.
+// split's dW partials).  Block = 16 split-slices x 16 float4 columns: every thread streams
+// S/16 rows of one 16-byte column, the 16 slices are summed through LDS in slice order.  (The
+// first form, 4 slices x 64 columns, launched 181 blocks for a growth conv's 46 K weights —
+// under one per CU — and each thread walked S/4 = 16..64 dependent rows: ~20 us per reduce,
+// latency-bound, on the side stream beside the RDB gather convs.)
+constexpr int RED_SL = 16, RED_COLS = 16;
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
-    __shared__ f32x4 red[4][64];
+    __shared__ f32x4 red[RED_SL][RED_COLS];
     const isr_wgrad_desc& d = a.d;
     const size_t per = (size_t)9 * d.cout * d.cin;
     const size_t row = per + d.cout;
     const int nv = (int)(row / 4);
-    const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int slice = threadIdx.x >> 6;
+    const int lc = threadIdx.x % RED_COLS, slice = threadIdx.x / RED_COLS;
+    const int col = blockIdx.x * RED_COLS + lc;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (col < nv) {
         const f32x4* src = reinterpret_cast<const f32x4*>(a.ws) + col;
 #pragma unroll 4
-        for (int sp = slice; sp < a.splits; sp += 4) acc += src[(size_t)sp * (row / 4)];
+        for (int sp = slice; sp < a.splits; sp += RED_SL) acc += src[(size_t)sp * (row / 4)];
     }
-    red[slice][threadIdx.x & 63] = acc;
+    red[slice][lc] = acc;
     __syncthreads();
     if (slice != 0 || col >= nv) return;
-    acc = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    acc = red[0][lc];
+#pragma unroll
+    for (int k = 1; k < RED_SL; ++k) acc += red[k][lc];
     const int cs4 = d.cout >> 2;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -419,7 +424,7 @@ static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipS
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     const size_t nv = ((size_t)9 * d->cout * d->cin + d->cout) / 4;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nv + 63) / 64)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nv + RED_COLS - 1) / RED_COLS)), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
