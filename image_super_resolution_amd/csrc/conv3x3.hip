@@ -114,6 +114,12 @@ struct C3 {
 
 template <int V> struct IC { static constexpr int value = V; };
 
+// 1: s_setprio 1 around each chunk's MFMA steps (as the trunk kernel): measured slower on the
+// SRGAN step, 54.43 / 54.53 vs 53.95 / 54.21 ms same box (profiles/r03_train_conv_prio_ab.jsonl)
+#ifndef ISR_CONV_PRIO
+#define ISR_CONV_PRIO 0
+#endif
+
 // A operand of the residual fold: (1/s1) I on couts [16 h16, 16 h16 + 16) of a 32-cout
 // fragment (lane l supplies A[l & 31][8 (l >> 5) .. + 8]); trunk.hip builds the same.
 __device__ __forceinline__ uint32_t fold_idv(float s1) {  // bf16 bits of 1/s1, in an SGPR
@@ -541,7 +547,10 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
-    #pragma unroll
+    #if ISR_CONV_PRIO
+            __builtin_amdgcn_s_setprio(1);  // A/B: the MFMA steps ahead of the co-resident block's issue
+#endif
+#pragma unroll
             for (int st = 0; st < NS; ++st) {
                 const int cur = C::PIPE ? (st & 1) : 0;
                 if constexpr (C::SPL > 1) {
@@ -613,6 +622,9 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
                     }
                 }
             }
+#if ISR_CONV_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
     };
     int chunk0 = 0;
     if constexpr (C::FOLD && C::NF == 2 && C::KS == 1 && C::TN == 3) {
