@@ -181,8 +181,9 @@ __device__ __forceinline__ bool rec_fold(const_rec_t& r) { return ((r.deps >> 8)
 __device__ __forceinline__ uint32_t rec_idv(const_rec_t& r) { return r.deps >> 16; }
 
 // Tuning builds: ablation knobs (timing only, outputs wrong): bit 1 = no halo LDS-DMA after the
-// first item, 4 = no epilogue stores; [1] = workgroups per CU (host side, 0 = occupancy).  (An
-// MFMA ablation branch inside the step loop would cut the MFMA/read schedule into blocks.)
+// first item, 4 = no epilogue stores, 8 = no weight LDS-DMA, 16 = no dependency waits;
+// [1] = workgroups per CU (host side, 0 = occupancy).  (An MFMA ablation branch inside the step
+// loop would cut the MFMA/read schedule into blocks.)
 #ifdef ISR_TUNING
 __device__ int g_trunk_knobs[4];
 static int g_trunk_per_cu = 0;
@@ -372,7 +373,7 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
 #pragma unroll
     for (int k = 0; k < WPW; ++k) {
         const int j = wave + WM * k;
-        if (j < s.wpc) {
+        if (j < s.wpc && !(abl & 8)) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, ISR_LDS_PTR(wd + j * 1024), 16, lane * 16, wo + j * 1024, 0, 0);
             ++n;
         }
@@ -613,7 +614,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     auto wait_deps = [&](int tt, unsigned nd) {
         force_publish(c, st);
         trunk_stamp(L, t, c.ntiles, 4);
-        dep_wait(c.state, nb_of(tt, c.nbx, c.nby), nd, c.gen);
+        if (!(c.abl & 16)) dep_wait(c.state, nb_of(tt, c.nbx, c.nby), nd, c.gen);
         if (c.acquire) acquire_fence();
         trunk_stamp(L, t, c.ntiles, 5);
     };

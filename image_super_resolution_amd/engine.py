@@ -19,6 +19,7 @@ BatchNorm is folded into the conv (fuse_conv_and_bn, :366-406) at pack time.
 from __future__ import annotations
 
 import ctypes
+import warnings
 from dataclasses import dataclass, field
 
 import torch
@@ -192,7 +193,9 @@ class GeneratorPlan:
             # dependencies instead of 240 kernel boundaries
             try:
                 self.chain = ConvChain([d for _, d, _, _ in L[trunk0:]], X, device, acquire=chain_acquire)
-            except ValueError:  # e.g. buffers beyond the 2 GiB descriptor window: per-conv launches
+            except ValueError as e:  # e.g. buffers beyond the 2 GiB descriptor window: per-conv launches
+                warnings.warn(f"RRDB trunk on 240 per-conv launches instead of the persistent trunk kernel: {e}",
+                              stacklevel=2)
                 self.chain = None
             if self.chain is not None:
                 L[trunk0:] = [(self.chain.fn, self.chain.desc, ("chain", len(L) - trunk0), None)]
@@ -283,6 +286,8 @@ class ConvChain:
         if grid.t.numel() * 2 >= 2 ** 31:
             raise ValueError("conv chain: activation buffers must stay below 2 GiB (buffer-descriptor window)")
         self.variant = CHAIN_VARIANT if variant is None else variant
+        if self.variant == 3 and grid.ha % 32:
+            raise ValueError("conv chain: variant 3 (32x32 trunk tiles) needs the padded height a multiple of 32")
         raw = b"".join(bytes(d) for d in descs)
         self._table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
         self._kinds = torch.tensor(kinds, dtype=torch.int32, device=device)

@@ -23,6 +23,7 @@ halo=0 mode:
 from __future__ import annotations
 
 import heapq
+import warnings
 from collections import defaultdict
 from dataclasses import dataclass
 from typing import Callable, Sequence
@@ -92,11 +93,12 @@ def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | N
     extended by `halo` LR rows above and below (clipped to the image, like a window's halo);
     rank r takes the k contiguous bands [r k, (r + 1) k).  k is the smallest count that keeps a
     band's input within `max_rows` (the persistent trunk kernel's 2 GiB buffer window by
-    default, see band_max_rows).  Every band of a rank has one of at most two input shapes (an
-    interior band, an image-edge band), so a rank builds <= 2 plans and runs each band as ONE
-    batch-1 forward over the full width — instead of the 3-4 window shapes at batch 1-2 an LPT
-    deal of rs.py windows gives it, and with no vertical seams.  Returns per-rank Tile lists
-    (Tile.x = 0, Tile.w = width)."""
+    default, see band_max_rows).  EVERY band has the same input height, min(height, core +
+    2 halo): an image-edge band (halo clipped at the edge) or the ragged last band extends its
+    input further into the image instead (more context than the halo asks, never less), so a
+    rank builds ONE plan for all its bands and runs each as one batch-1 forward over the full
+    width — instead of the 3-4 window shapes at batch 1-2 an LPT deal of rs.py windows gives
+    it, and with no vertical seams.  Returns per-rank Tile lists (Tile.x = 0, Tile.w = width)."""
     if world < 1 or halo < 0 or height < 1 or width < 1:
         raise ValueError("plan_bands: world >= 1, halo >= 0 and a non-empty image required")
     if max_rows is None:
@@ -107,10 +109,12 @@ def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | N
         if core + 2 * halo <= max_rows or core == 1:
             break
         k += 1
+    rows = min(height, core + 2 * halo)  # the one input height of every band
     bands: list[Tile] = []
     for y in range(0, height, core):
         h = min(core, height - y)
-        bands.append(Tile(len(bands), y, 0, h, width, max(0, y - halo), 0, min(height, y + h + halo), width))
+        y0 = min(max(0, y - halo), height - rows)
+        bands.append(Tile(len(bands), y, 0, h, width, y0, 0, y0 + rows, width))
     out: list[list[Tile]] = [[] for _ in range(world)]
     per = -(-len(bands) // world)
     for b in bands:
@@ -218,13 +222,20 @@ class TileUpscaler:
         """`shard`: "windows" runs rs.py's windows (dealt longest-processing-time-first over
         ranks, shard_tiles; the canvas equals the single-rank one bit for bit); "bands" runs
         full-width horizontal bands with the same halo (plan_bands: one rank's share is one or a
-        few bands of at most two shapes, one forward each; on one GPU the image splits into as
-        few bands as the trunk kernel's 2 GiB buffer window allows; needs halo > 0 to hide its
-        seams, and differs from the windowed canvas by the seams each form leaves)."""
+        few bands of one input shape, one batch-1 forward each — `batch` applies to windows only;
+        on one GPU the image splits into as few bands as the trunk kernel's 2 GiB buffer window
+        allows; needs halo > 0 to hide its seams, and differs from the windowed canvas by the
+        seams each form leaves)."""
         if batch < 1:
             raise ValueError("batch must be >= 1")
         if shard not in ("windows", "bands"):
             raise ValueError(f"shard must be 'windows' or 'bands', got {shard!r}")
+        if shard == "bands" and halo == 0:
+            warnings.warn("shard='bands' with halo=0: the bands' seams are not hidden (pass halo > 0)",
+                          stacklevel=2)
+        if shard == "bands" and batch != 1:
+            warnings.warn(f"shard='bands' runs every band as one batch-1 forward; batch={batch} is ignored",
+                          stacklevel=2)
         self.runner, self.scale, self.window, self.halo, self.batch = runner, scale, window, halo, batch
         self.device = torch.device(device)
         self.shard = shard

@@ -554,8 +554,8 @@ class _Buckets:
     """The data-parallel gradient all-reduce of one backward, overlapped with it (SURVEY.md §8e,
     DDP's bucketed all-reduce): the flat fp32 gradient buffer's segments complete in backward
     order (tail, RRDB nb-1 .. 0, head); consecutive segments merge into buckets of >=
-    BUCKET_BYTES, and each bucket is all-reduced on a communication stream as soon as the stream
-    that produced its last segment (main, or the side stream of the RDB weight gradients) has
+    BUCKET_BYTES, and each bucket is all-reduced on a communication stream as soon as every stream
+    that produced one of its segments (main, or the side stream of the RDB weight gradients) has
     enqueued it — an event hand-off, no host synchronisation.  finish() makes the main stream
     wait for every bucket and divides by the world size.  Same sums as one flat all-reduce per
     element (each element is reduced exactly once), so ranks stay bitwise equal."""
@@ -566,6 +566,7 @@ class _Buckets:
         self.group = None if group is True else group
         self.comm = plan.__dict__.setdefault("_comm_stream", torch.cuda.Stream(grads.device))
         self.lo = self.hi = None
+        self.producers = []  # streams that wrote the pending bucket's segments
         self.works = []
 
     def ready(self, seg_id, stream) -> None:
@@ -575,13 +576,19 @@ class _Buckets:
         else:
             assert hi == self.lo, "gradient segments must complete in descending buffer order"
             self.lo = lo
+        if not any(s is stream for s in self.producers):
+            self.producers.append(stream)
         if (self.hi - self.lo) * 4 >= BUCKET_BYTES or seg_id == "head":
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            self.comm.wait_event(ev)
+            # a merged bucket can hold segments of both streams (side-stream RDB weight
+            # gradients beside main-stream head/tail ones): wait for every producer
+            for s in self.producers:
+                ev = torch.cuda.Event()
+                ev.record(s)
+                self.comm.wait_event(ev)
             with torch.cuda.stream(self.comm):
                 self._reduce(self.grads[self.lo:self.hi])
             self.lo = self.hi = None
+            self.producers = []
 
     def _reduce(self, t: torch.Tensor) -> None:
         dist = self.dist

@@ -343,8 +343,10 @@ int isr_conv3x3_check(const isr_conv_desc* d);
  * `state` (device, isr_conv_chain_state_words(n, ha, wa) uint32 words, zeroed ONCE by the
  * caller before first use, then owned by the library across calls: a generation counter in
  * state[0] replaces per-call zeroing); after a call, state[1] == state[0] means a dependency
- * wait gave up (results invalid — not expected unless the device is shared); state[2] counts
- * give-ups over all launches (never reset: a host remembers the last count it saw).  nl < 1024.
+ * wait gave up (results invalid — not expected unless the device is shared); state[2] is a
+ * sticky give-up counter that only grows (never reset): ANY change since the last value a host
+ * saw means a launch in between gave up (one add per giving-up wave or refused launch, so it
+ * is not a count of failed launches).  1 <= nl <= 1024.
  * acquire = 1 adds an agent-scope acquire before each tile's loads (otherwise the
  * hand-off relies on sc1 loads). */
 typedef struct isr_chain_desc {
@@ -373,7 +375,8 @@ int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_
  * wait met; s_memrealtime ticks, 100 MHz); NULL stops. */
 int isr_tuning_trunk_stamps(void* buf);
 /* Tuning builds only: ablations of later production chain launches (timing only, outputs wrong):
- * bit 1 = no halo LDS-DMA after the first chunk, 2 = no MFMAs, 4 = no epilogue stores;
+ * bit 1 = no halo LDS-DMA, 4 = no epilogue stores, 8 = no weight LDS-DMA, 16 = no dependency
+ * waits;
  * per_cu > 0 caps the resident workgroups per CU (the grid). */
 int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k3);
 /* Tuning builds only: per-item cycle stamps (s_memtime) of later production chain launches into

@@ -64,12 +64,14 @@ class _PerRankD(torch.nn.Module):
         return torch.cat([self.d(c.contiguous()) for c in x.chunk(self.parts)])
 
 
-def _worker(rank, world, port, mode, tmp, q):
+def _worker(rank, world, port, mode, tmp, q, bucket_mb="0"):
     sys.path.insert(0, str(ROOT))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    # every backward segment (tail, each RRDB, head) its own all-reduce bucket, so the overlapped
-    # bucket schedule (train_engine._Buckets) is exercised at this tiny depth
-    os.environ["ISR_DDP_BUCKET_MB"] = "0"
+    # "0": every backward segment (tail, each RRDB, head) its own all-reduce bucket, so the
+    # overlapped bucket schedule (train_engine._Buckets) is exercised at this tiny depth; "8"
+    # (the default size): one merged bucket holding main-stream (tail, head) AND side-stream
+    # (RRDB weight gradients) segments, whose all-reduce must wait for both streams
+    os.environ["ISR_DDP_BUCKET_MB"] = bucket_mb
     try:
         import torch.distributed as dist
 
@@ -120,11 +122,11 @@ def _worker(rank, world, port, mode, tmp, q):
         raise
 
 
-def _run(mode, world, tmp):
+def _run(mode, world, tmp, bucket_mb="0"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, str(tmp), q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, str(tmp), q, bucket_mb)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
@@ -153,9 +155,9 @@ def _delta_close(a, b, p0, rel_max, cos_min, what):
     print(f"{what}: worst parameter-change rel {worst[0]:.3e} (cos {worst[1]:.5f}) at {worst[2]}")
 
 
-@pytest.mark.parametrize("mode", ["res", "srgan"])
-def test_two_rank_data_parallel_matches(mode, tmp_path):
-    dp = _run(mode, 2, tmp_path / "dp")
+@pytest.mark.parametrize("mode,bucket_mb", [("res", "0"), ("srgan", "0"), ("res", "8")])
+def test_two_rank_data_parallel_matches(mode, bucket_mb, tmp_path):
+    dp = _run(mode, 2, tmp_path / "dp", bucket_mb)
     single = _run(mode, 1, tmp_path / "single")[0]
     # rank 1 started from other weights; after broadcast + 2 averaged steps both ranks agree bitwise
     np.testing.assert_array_equal(np.concatenate([v.ravel() for v in dp[0]["p0"].values()]),

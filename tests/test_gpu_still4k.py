@@ -154,7 +154,7 @@ def test_cfg4_bands_vs_whole_image(setup):
     """Each of 8 ranks' bands (one 334- or 302-row full-width band per rank) run on this GPU,
     stitched: the canvas rank 0 would assemble, against one whole-image forward."""
     r = setup["runner"]
-    up = tiler.TileUpscaler(r, S, window=WINDOW, halo=HALO, batch=4, device=DEV, shard="bands")
+    up = tiler.TileUpscaler(r, S, window=WINDOW, halo=HALO, batch=1, device=DEV, shard="bands")
     img = setup["img"].to(DEV)
     shards = up.shards(H, W, 8)
     assert all(len({t.in_shape for t in lst}) == 1 for lst in shards)
@@ -183,7 +183,7 @@ def test_bands_with_full_receptive_halo_equal_whole_image_bitwise():
     img = torch.randint(0, 256, (3, 150, 230), generator=g, dtype=torch.uint8).to(DEV)
     runner = tiler.runner_for(m, DEV)
     whole = m(img[None])[0]
-    up = tiler.TileUpscaler(runner, S, window=64, halo=24, batch=2, device=DEV, shard="bands")
+    up = tiler.TileUpscaler(runner, S, window=64, halo=24, batch=1, device=DEV, shard="bands")
     for world in (2, 3):
         shards = up.shards(150, 230, world)
         done = {}
