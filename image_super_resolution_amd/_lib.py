@@ -147,6 +147,9 @@ SIGNATURES = {
     "isr_clip_coef": (c_int32, [c_void_p, c_int32, c_float, c_void_p, c_void_p]),
     "isr_mt_scale": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "isr_mt_lerp": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p]),
+    "isr_mt_adam_guarded": (c_int32, [c_void_p, c_void_p, c_int32, POINTER(IsrAdamArgs), c_void_p, c_void_p,
+                                      c_void_p]),
+    "isr_mt_lerp_guarded": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p]),
     "isr_last_error": (ctypes.c_char_p, []),
     "isr_version": (c_int32, []),
 }

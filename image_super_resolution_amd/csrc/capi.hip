@@ -43,11 +43,11 @@ size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
 int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
 int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s);
 int mt_adam_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, const isr_adam_args* a,
-                     const float* scale, hipStream_t s);
+                     const float* scale, const uint32_t* guard, hipStream_t s);
 int mt_sumsq_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, float* partial, hipStream_t s);
 int clip_coef_dispatch(const float* partial, int n, float max_norm, float* out, hipStream_t s);
 int mt_axpby_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, int mode, const float* coef, float d,
-                      hipStream_t s);
+                      const uint32_t* guard, hipStream_t s);
 }  // namespace isr
 
 static thread_local char g_err[512] = "";
@@ -106,13 +106,18 @@ static int mt_ok(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, con
     return ISR_OK;
 }
 
-int isr_mt_adam(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, const isr_adam_args* a,
-                const float* scale, isr_stream_t s) {
+int isr_mt_adam_guarded(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, const isr_adam_args* a,
+                        const float* scale, const uint32_t* guard, isr_stream_t s) {
     if (int rc = mt_ok(ts, cs, n, "mt_adam")) return rc;
     if (!a) return fail(ISR_ERR_BAD_DESC, "mt_adam: null args");
     if (!(a->bc2_sqrt > 0.f) || !(a->beta1 >= 0.f && a->beta1 < 1.f) || !(a->beta2 >= 0.f && a->beta2 < 1.f))
         return fail(ISR_ERR_BAD_DESC, "mt_adam: bad betas / bias correction");
-    return launched(isr::mt_adam_dispatch(ts, cs, n, a, scale, (hipStream_t)s), "mt_adam");
+    return launched(isr::mt_adam_dispatch(ts, cs, n, a, scale, guard, (hipStream_t)s), "mt_adam");
+}
+
+int isr_mt_adam(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, const isr_adam_args* a,
+                const float* scale, isr_stream_t s) {
+    return isr_mt_adam_guarded(ts, cs, n, a, scale, nullptr, s);
 }
 
 int isr_mt_sumsq(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, float* partial, isr_stream_t s) {
@@ -129,12 +134,17 @@ int isr_clip_coef(const float* partial, int32_t n, float max_norm, float* out, i
 int isr_mt_scale(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, const float* coef, isr_stream_t s) {
     if (int rc = mt_ok(ts, cs, n, "mt_scale")) return rc;
     if (!coef) return fail(ISR_ERR_BAD_DESC, "mt_scale: null coefficient");
-    return launched(isr::mt_axpby_dispatch(ts, cs, n, 0, coef, 0.f, (hipStream_t)s), "mt_scale");
+    return launched(isr::mt_axpby_dispatch(ts, cs, n, 0, coef, 0.f, nullptr, (hipStream_t)s), "mt_scale");
+}
+
+int isr_mt_lerp_guarded(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, float d, const uint32_t* guard,
+                        isr_stream_t s) {
+    if (int rc = mt_ok(ts, cs, n, "mt_lerp")) return rc;
+    return launched(isr::mt_axpby_dispatch(ts, cs, n, 1, nullptr, d, guard, (hipStream_t)s), "mt_lerp");
 }
 
 int isr_mt_lerp(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int32_t n, float d, isr_stream_t s) {
-    if (int rc = mt_ok(ts, cs, n, "mt_lerp")) return rc;
-    return launched(isr::mt_axpby_dispatch(ts, cs, n, 1, nullptr, d, (hipStream_t)s), "mt_lerp");
+    return isr_mt_lerp_guarded(ts, cs, n, d, nullptr, s);
 }
 int isr_version(void) { return 1; }
 

@@ -32,8 +32,17 @@ struct AdamOp {
     }
 };
 
+// guard (nullable): two words written by an earlier launch of the stream (the trunk kernel's
+// sticky give-up count and the count the host has accepted, isr_chain_desc state[2] / [3]);
+// a block skips its chunk when they differ, so a failed forward never reaches the parameters.
+__device__ __forceinline__ bool mt_guarded_out(const uint32_t* guard) {
+    return guard != nullptr && guard[0] != guard[1];
+}
+
 __global__ __launch_bounds__(MT_THREADS) void mt_adam_kernel(const isr_mt_tensor* __restrict__ ts,
-                                                             const isr_mt_chunk* __restrict__ cs, AdamOp op) {
+                                                             const isr_mt_chunk* __restrict__ cs, AdamOp op,
+                                                             const uint32_t* __restrict__ guard) {
+    if (mt_guarded_out(guard)) return;
     const isr_mt_chunk c = cs[blockIdx.x];
     const isr_mt_tensor t = ts[c.t];
     const float s = op.scale ? *op.scale : 1.f;
@@ -116,7 +125,9 @@ __global__ __launch_bounds__(MT_THREADS) void clip_coef_kernel(const float* __re
 // g *= *coef  (mode 0)   |   p = p*d + (1-d)*g  (mode 1: EMA, p = ema tensor, g = model tensor)
 __global__ __launch_bounds__(MT_THREADS) void mt_axpby_kernel(const isr_mt_tensor* __restrict__ ts,
                                                               const isr_mt_chunk* __restrict__ cs, int mode,
-                                                              const float* __restrict__ coef, float d) {
+                                                              const float* __restrict__ coef, float d,
+                                                              const uint32_t* __restrict__ guard) {
+    if (mt_guarded_out(guard)) return;
     const isr_mt_chunk c = cs[blockIdx.x];
     const isr_mt_tensor t = ts[c.t];
     if (mode == 0) {
@@ -153,8 +164,8 @@ __global__ __launch_bounds__(MT_THREADS) void mt_axpby_kernel(const isr_mt_tenso
 }
 
 int mt_adam_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, const isr_adam_args* a,
-                     const float* scale, hipStream_t s) {
-    hipLaunchKernelGGL(mt_adam_kernel, dim3(n), dim3(MT_THREADS), 0, s, ts, cs, AdamOp{*a, scale});
+                     const float* scale, const uint32_t* guard, hipStream_t s) {
+    hipLaunchKernelGGL(mt_adam_kernel, dim3(n), dim3(MT_THREADS), 0, s, ts, cs, AdamOp{*a, scale}, guard);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -169,8 +180,8 @@ int clip_coef_dispatch(const float* partial, int n, float max_norm, float* out, 
 }
 
 int mt_axpby_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, int mode, const float* coef, float d,
-                      hipStream_t s) {
-    hipLaunchKernelGGL(mt_axpby_kernel, dim3(n), dim3(MT_THREADS), 0, s, ts, cs, mode, coef, d);
+                      const uint32_t* guard, hipStream_t s) {
+    hipLaunchKernelGGL(mt_axpby_kernel, dim3(n), dim3(MT_THREADS), 0, s, ts, cs, mode, coef, d, guard);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -315,11 +315,20 @@ class ConvChain:
         """Enqueue (current stream) an async copy of the give-up count into pinned `dst` (int32[1])."""
         dst.copy_(self.state[2:3], non_blocking=True)
 
+    @property
+    def guard_ptr(self) -> int:
+        """Device address of state words [2, 3] (the sticky give-up count, the count the host has
+        accepted): the guard of optim's HIP Adam / EMA updates (isr_mt_adam_guarded)."""
+        return self.state.data_ptr() + 8
+
     def check_count(self, count: int) -> None:
-        """Raise ChainFailed when `count` (a snapshot) shows a give-up not yet reported."""
+        """Raise ChainFailed when `count` (a snapshot) shows a give-up not yet reported; the
+        reported count becomes the accepted one (state[3]), so guarded optimiser updates of
+        launches after it run again once the caller has handled the error."""
         seen = getattr(self, "_fails_seen", 0)
         if count != seen:
             self._fails_seen = count
+            self.state[3:4].fill_(count)
             raise ChainFailed("conv chain: a dependency wait gave up (launch not fully resident); "
                               "outputs of that forward are invalid")
 

@@ -16,6 +16,7 @@ their grad / state; the kernels treat each as a flat run of numel floats.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 
@@ -108,6 +109,24 @@ def _check(t: torch.Tensor, what: str):
         raise ValueError(f"{what}: tensor must be dense (contiguous or channels_last)")
 
 
+# The trunk give-up guard of the step being applied (a device pointer to the trunk state's words
+# [2] (sticky give-up count) and [3] (the count the host accepted), engine.ConvChain.guard_ptr),
+# or None.  Set by the trainer around each step's optimiser / EMA updates (step_guard); the HIP
+# Adam and EMA kernels then skip their update on the device when the two words differ.
+_GUARD: list = [None]
+
+
+@contextlib.contextmanager
+def step_guard(ptr):
+    """Guard every FusedAdam.step / ema_update_ enqueued inside with the trunk state at `ptr`
+    (None: unguarded)."""
+    prev, _GUARD[0] = _GUARD[0], ptr
+    try:
+        yield
+    finally:
+        _GUARD[0] = prev
+
+
 class FusedAdam(torch.optim.Optimizer):
     """torch.optim.Adam (amsgrad=False, maximize=False) as one HIP launch per
     parameter group and step (isr_mt_adam)."""
@@ -153,8 +172,8 @@ class FusedAdam(torch.optim.Optimizer):
                 bc1 = 1.0 - b1 ** t
                 a = _lib.IsrAdamArgs(step=-group["lr"] / bc1, beta1=b1, beta2=b2, eps=group["eps"],
                                      weight_decay=group["weight_decay"], bc2_sqrt=math.sqrt(1.0 - b2 ** t))
-                _lib.check(lib.isr_mt_adam(pt.data_ptr(), ch.data_ptr(), n, ctypes.byref(a),
-                                           None, ops._stream()), "isr_mt_adam")
+                _lib.check(lib.isr_mt_adam_guarded(pt.data_ptr(), ch.data_ptr(), n, ctypes.byref(a),
+                                                   None, _GUARD[0], ops._stream()), "isr_mt_adam")
                 ops.bump_param_epoch()  # packed-weight caches must repack (raw-pointer writes)
         return loss
 
@@ -207,5 +226,6 @@ def ema_update_(ema: list[torch.Tensor], model: list[torch.Tensor], d: float) ->
             keep.append(m)  # alive until the launch is enqueued (stream-ordered reuse after that)
         rows.append((v.data_ptr(), m.data_ptr(), 0, 0, v.numel()))
     pt, ch, n = _EMA_CACHE.get(rows, ema[0].device)
-    _lib.check(_lib.load().isr_mt_lerp(pt.data_ptr(), ch.data_ptr(), n, float(d), ops._stream()), "isr_mt_lerp")
+    _lib.check(_lib.load().isr_mt_lerp_guarded(pt.data_ptr(), ch.data_ptr(), n, float(d), _GUARD[0],
+                                                ops._stream()), "isr_mt_lerp")
     ops.bump_param_epoch()

@@ -647,6 +647,14 @@ def verify_chains(gen: nn.Module) -> None:
         chain.verify()
 
 
+def step_guard_ptr(gen: nn.Module):
+    """The trunk give-up guard of the generator's last training forward (engine.ConvChain.guard_ptr),
+    or None when it ran without the persistent trunk kernel."""
+    plan = gen.__dict__.get("_isr_train_plan")
+    chain = getattr(plan, "chain", None)
+    return chain.guard_ptr if chain is not None else None
+
+
 def get_train_plan(gen: nn.Module, x: torch.Tensor) -> GeneratorTrainPlan:
     n, _, h, w = x.shape
     key = (n, h, w, str(x.device))

@@ -19,6 +19,9 @@ Differences, all deliberate:
   so its discarded parameter gradients (train.py:102, zeroed at :119) are not computed.
 * loss.item() host syncs happen once per `log_every` iterations instead of
   every iteration (train.py:64-65, :101-112).
+* a forward whose persistent trunk kernel gave up (engine.ChainFailed, reported at the latest
+  at epoch end) changes no parameter: every Adam / EMA update of that step and of later steps
+  is skipped on the device (optim.step_guard) until the host has reported the failure.
 * multi-GPU (one process per GPU): the generator's gradients are averaged by
   one RCCL all-reduce of its flat gradient buffer inside the HIP backward
   (train_engine.enable_grad_allreduce); the discriminator's by one flat
@@ -32,7 +35,8 @@ import time
 import torch
 from .models import ModelEMA
 from .optim import clip_grad_norm_  # HIP multi-tensor clip (same signature as torch's)
-from .train_engine import allreduce_grads
+from .optim import step_guard
+from .train_engine import allreduce_grads, step_guard_ptr
 
 
 def _scalar(writer, tag, value, step):
@@ -73,10 +77,11 @@ def train(model, ema: ModelEMA, batches, transform, compute_loss, optimizer, gra
         gradscaler.scale(loss).backward()
         gradscaler.unscale_(optimizer)
         clip_grad_norm_(model.parameters(), 10)
-        gradscaler.step(optimizer)
-        gradscaler.update()
-        schedule.step()
-        ema.update(_unwrap(model))
+        with step_guard(step_guard_ptr(_unwrap(model))):  # a failed trunk forward updates nothing
+            gradscaler.step(optimizer)
+            gradscaler.update()
+            schedule.step()
+            ema.update(_unwrap(model))
         pending.append(loss.detach())
         if len(pending) == log_every or idx == total - 1:
             vals = torch.stack(pending).cpu().tolist()
@@ -127,10 +132,12 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
         gradscaler_gen.scale(perceptual_loss).backward()
         gradscaler_gen.unscale_(optimizer_g)
         clip_grad_norm_(gen_net.parameters(), 10)
-        gradscaler_gen.step(optimizer_g)
-        gradscaler_gen.update()
-        schedule_g.step()
-        ema.update(_unwrap(gen_net))
+        guard = step_guard_ptr(_unwrap(gen_net))  # a failed trunk forward updates neither G nor D
+        with step_guard(guard):
+            gradscaler_gen.step(optimizer_g)
+            gradscaler_gen.update()
+            schedule_g.step()
+            ema.update(_unwrap(gen_net))
 
         with torch.autocast("cuda", dtype=torch.bfloat16):
             sr_discriminated = dis_net(sr_images.detach())
@@ -142,9 +149,10 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
             allreduce_grads(dis_net.parameters(), None if dist_group is True else dist_group)
         gradscaler_dis.unscale_(optimizer_d)
         clip_grad_norm_(dis_net.parameters(), 10)
-        gradscaler_dis.step(optimizer_d)
-        gradscaler_dis.update()
-        schedule_d.step()
+        with step_guard(guard):
+            gradscaler_dis.step(optimizer_d)
+            gradscaler_dis.update()
+            schedule_d.step()
         pending.append(torch.stack([content_loss.detach(), adversarial_loss_.detach(), adversarial_loss.detach()]))
         if len(pending) == log_every or idx == total - 1:
             vals = torch.stack(pending).cpu().tolist()

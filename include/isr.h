@@ -346,7 +346,8 @@ int isr_conv3x3_check(const isr_conv_desc* d);
  * wait gave up (results invalid — not expected unless the device is shared); state[2] is a
  * sticky give-up counter that only grows (never reset): ANY change since the last value a host
  * saw means a launch in between gave up (one add per giving-up wave or refused launch, so it
- * is not a count of failed launches).  1 <= nl <= 1024.
+ * is not a count of failed launches); state[3] belongs to the host (the library never writes it:
+ * isr_mt_adam_guarded / isr_mt_lerp_guarded compare it with state[2]).  1 <= nl <= 1024.
  * acquire = 1 adds an agent-scope acquire before each tile's loads (otherwise the
  * hand-off relies on sc1 loads). */
 typedef struct isr_chain_desc {
@@ -434,6 +435,15 @@ int isr_mt_scale(const isr_mt_tensor* tensors, const isr_mt_chunk* chunks, int32
                  isr_stream_t s);
 /* p = p*d + (1-d)*g over every chunk (ModelEMA.update: p = EMA tensor, g = model tensor). */
 int isr_mt_lerp(const isr_mt_tensor* tensors, const isr_mt_chunk* chunks, int32_t nchunks, float d, isr_stream_t s);
+/* The same two updates, skipped on the device (no host synchronisation) when guard[0] != guard[1]:
+ * pass `isr_chain_desc.state + 2` of the trunk launch that produced this step's forward (state[2]
+ * the sticky give-up counter, state[3] the count the host has accepted, zero-initialised with the
+ * state), so a forward whose dependency wait gave up never reaches the parameters or the EMA.
+ * guard = NULL is the unguarded call. */
+int isr_mt_adam_guarded(const isr_mt_tensor* tensors, const isr_mt_chunk* chunks, int32_t nchunks,
+                        const isr_adam_args* a, const float* scale, const uint32_t* guard, isr_stream_t s);
+int isr_mt_lerp_guarded(const isr_mt_tensor* tensors, const isr_mt_chunk* chunks, int32_t nchunks, float d,
+                        const uint32_t* guard, isr_stream_t s);
 
 const char* isr_last_error(void);
 int isr_version(void);

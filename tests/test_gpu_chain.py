@@ -159,3 +159,41 @@ def test_give_up_raises_from_video_and_tiler_before_output():
             c.state[2] += 1
     with pytest.raises(engine.ChainFailed):
         tu(img)
+
+
+def test_give_up_training_step_leaves_parameters_unchanged():
+    """A training forward whose trunk kernel gave up (simulated through the sticky count) must
+    not reach the parameters: trainer.train's Adam and EMA updates of that step are skipped on
+    the device (optim.step_guard → isr_mt_adam_guarded / isr_mt_lerp_guarded), the epoch-end
+    check raises ChainFailed, and once the host has reported it the next step updates again."""
+    from image_super_resolution_amd import optim, trainer
+    torch.manual_seed(0)
+    m = models.EResNet(1, 0.2, 4)
+    m.load_state_dict(synth_state_dict(m.state_dict(), 7))
+    m = m.to(DEV).train()
+    ema = models.ModelEMA(m, tau=100)
+    opt = optim.FusedAdam(m.parameters(), lr=1e-3)
+    sched = torch.optim.lr_scheduler.LinearLR(opt, 1.0, 0.5, 10)
+    sc = torch.amp.GradScaler("cuda", enabled=False)
+    lr, hr01 = synth_lr_batch(2, 24, 32, seed=3, scale=4)
+    batch = (hr01.to(DEV) * 2 - 1, normalize(lr).to(DEV))
+    ident = lambda b: b  # noqa: E731  (the batch is already (hr, lr))
+    loss = torch.nn.functional.mse_loss
+
+    def snap():
+        return ([p.detach().clone() for p in m.parameters()],
+                [v.detach().clone() for v in ema.ema.state_dict().values() if v.dtype.is_floating_point])
+
+    trainer.train(m, ema, [batch], ident, loss, opt, sc, sched, 0, steps=1)
+    plan = m.__dict__["_isr_train_plan"]
+    assert plan.chain is not None, "the training forward must run the trunk on the persistent kernel"
+    p0, e0 = snap()
+    plan.chain.state[2] += 1  # a give-up of the next forward's trunk launch
+    with pytest.raises(engine.ChainFailed):
+        trainer.train(m, ema, [batch], ident, loss, opt, sc, sched, 1, steps=1)
+    p1, e1 = snap()
+    for a, b in zip(p0 + e0, p1 + e1):
+        assert torch.equal(a, b), "a failed trunk forward changed a parameter or the EMA"
+    trainer.train(m, ema, [batch], ident, loss, opt, sc, sched, 2, steps=1)  # reported: updates resume
+    p2, _ = snap()
+    assert any(not torch.equal(a, b) for a, b in zip(p1, p2))
