@@ -433,7 +433,9 @@ class Model(nn.Module):
                 std = net[0].std.flatten().tolist()
                 x = inputs if inputs.dtype == torch.uint8 else inputs.float()
                 if x.dtype != torch.uint8:
-                    x = (x / net[0].max_pixel_value - net[0].mean) / net[0].std
+                    # Normalize divides by 255 for uint8 input only (utils/datasets.py:65-71):
+                    # float input is taken as already scaled
+                    x = (x - net[0].mean) / net[0].std
                 return engine.run_generator(gen._packed(inputs.device), x, out_u8=True, mean=mean, std=std)
         return net(inputs)
 

@@ -77,6 +77,28 @@ def test_model_u8_vs_reference_golden(golden):
 
 
 @torch.no_grad()
+def test_model_float_input_skips_the_255_division(golden):
+    """The reference's Normalize divides by 255 only for uint8 input (utils/datasets.py:65-71):
+    a float image already in [0, 1] is normalised as is, so it must give the uint8 image's
+    output (same normalised values up to fp32 rounding), and a float image in [0, 255] a
+    different one."""
+    g = golden("model_u8")
+    m = _model(lambda: models.ResNet(1, 0.2, scaleRate=4), int(g["seed"]))
+    wrapped = models.Model(m)
+    wrapped.init_normalize([0.485, 0.456, 0.406], [0.229, 0.224, 0.225])
+    wrapped = wrapped.eval().fuse().to(DEV)
+    xu8 = t(g["x"]).to(DEV)
+    y_u8 = wrapped(xu8)
+    y_f = wrapped(xu8.float() / 255.0)
+    assert y_f.dtype == torch.uint8 and y_f.shape == y_u8.shape
+    d = (y_f.int() - y_u8.int()).abs()
+    assert d.max().item() <= 1 and (d > 0).float().mean().item() < 0.01
+    # a [0, 255] float image is NOT divided by 255 (the reference's quirk): a different output
+    y_255 = wrapped(xu8.float())
+    assert (y_255.int() - y_u8.int()).abs().float().mean().item() > 5.0
+
+
+@torch.no_grad()
 def test_blocks_vs_reference_golden(golden):
     g = golden("blocks")
     x = t(g["x"]).to(DEV)
