@@ -70,6 +70,11 @@ class IsrEwDesc(ctypes.Structure):
                 ("sa", c_float), ("sb", c_float), ("mslope", c_float)]
 
 
+class IsrSrTransformDesc(ctypes.Structure):
+    _fields_ = [("crops", c_void_p), ("hr", c_void_p), ("lr", c_void_p), ("n", c_int32), ("t", c_int32),
+                ("scale", c_int32), ("hr_norm", c_int32), ("mean", c_float * 3), ("std", c_float * 3)]
+
+
 class IsrConvertDesc(ctypes.Structure):
     _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32), ("c", c_int32),
                 ("nchw", c_void_p), ("v", IsrView), ("scale", c_void_p), ("shift", c_void_p),
@@ -113,6 +118,7 @@ SIGNATURES = {
     "isr_wgrad9x9": (c_int32, [POINTER(IsrWgrad9Desc), c_void_p, c_size_t, c_void_p]),
     "isr_ew_combine": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
     "isr_pixel_shuffle2": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
+    "isr_sr_transform": (c_int32, [POINTER(IsrSrTransformDesc), c_void_p]),
     "isr_pixel_unshuffle2": (c_int32, [POINTER(IsrEwDesc), c_void_p]),
     "isr_bn_stats": (c_int32, [POINTER(IsrBnDesc), c_void_p]),
     "isr_bn_finalize": (c_int32, [POINTER(IsrBnDesc), c_void_p]),

@@ -33,6 +33,7 @@ int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale
 int conv3x3_pack_batch(const isr_pack_item* items, int n, hipStream_t s);
 int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s);
 int pixel_shuffle2_dispatch(const isr_ew_desc* d, hipStream_t s);
+int sr_transform_dispatch(const isr_sr_transform_desc* d, hipStream_t s);
 int pixel_unshuffle2_dispatch(const isr_ew_desc* d, hipStream_t s);
 int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s);
 int nchw_to_blocked_dispatch(const isr_convert_desc* d, hipStream_t s);
@@ -433,6 +434,16 @@ int isr_ew_combine(const isr_ew_desc* d, isr_stream_t s) {
     if (d->b.data && !view_ok(d->b, d->ha, d->wa, 0, d->c, "ew.b", 1)) return ISR_ERR_BAD_DESC;
     if (d->m.data && !view_ok(d->m, d->ha, d->wa, 0, d->c, "ew.m", 1)) return ISR_ERR_BAD_DESC;
     return launched(isr::ew_combine_dispatch(d, (hipStream_t)s), "ew_combine");
+}
+
+int isr_sr_transform(const isr_sr_transform_desc* d, isr_stream_t s) {
+    if (!d || !d->crops || !d->hr || !d->lr) return fail(ISR_ERR_BAD_DESC, "sr_transform: null descriptor / buffer");
+    if (d->scale < 2 || d->scale > 4) return fail(ISR_ERR_UNSUPPORTED, "sr_transform: scale %d not in {2, 3, 4}", d->scale);
+    if (d->n <= 0 || d->t <= 0 || d->t % d->scale || (long long)d->n * 3 * d->t * d->t >= (1ll << 31))
+        return fail(ISR_ERR_BAD_DESC, "sr_transform: bad batch n=%d t=%d scale=%d", d->n, d->t, d->scale);
+    for (int c = 0; c < 3; ++c)
+        if (!(d->std[c] != 0.f)) return fail(ISR_ERR_BAD_DESC, "sr_transform: std[%d] is zero", c);
+    return launched(isr::sr_transform_dispatch(d, (hipStream_t)s), "sr_transform");
 }
 
 int isr_pixel_shuffle2(const isr_ew_desc* d, isr_stream_t s) {

@@ -505,3 +505,61 @@ int bn_dispatch(const isr_bn_desc* d, int op, hipStream_t s) {
 }
 
 }  // namespace isr
+
+namespace isr {
+
+// SR_dataset's per-sample transform (utils/datasets.py:344-355), batched on the device in ONE
+// pass over the uint8 crops: one thread per (image, LR pixel) reads its scale x scale HR block of
+// every channel, writes those HR pixels (PIL_to_tanh 2x/255 - 1, or Normalize in SRGAN mode) and
+// the LR pixel: OpenCV's uint8 INTER_LINEAR resize at an integer factor (odd: the block's centre
+// pixel; even: its centre 2x2 mean rounded half up — cv2's 11-bit fixed point at weights 0 / 0.5 /
+// 1, oracle.ref_cpu.cv2_resize_linear_u8; x2 is cv2's INTER_AREA, the same 2x2 mean), then
+// Normalize.  Same float formulas as data.GPUTransform's CPU form.
+template <int S>
+__global__ __launch_bounds__(256) void sr_transform_kernel(isr_sr_transform_desc d) {
+    const int t = d.t, lt = t / S;
+    const uint32_t total = (uint32_t)d.n * lt * lt;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const int lx = (int)(i % lt), tmp = (int)(i / lt), ly = tmp % lt, img = tmp / lt;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const size_t plane = (size_t)img * 3 + c;
+            const uint8_t* src = d.crops + (plane * t + (size_t)ly * S) * t + (size_t)lx * S;
+            float* hr = d.hr + (plane * t + (size_t)ly * S) * t + (size_t)lx * S;
+            const float mean = d.mean[c], stdv = d.std[c];
+            uint32_t u[S][S];
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+#pragma unroll
+                for (int k = 0; k < S; ++k) u[r][k] = src[(size_t)r * t + k];
+#pragma unroll
+                for (int k = 0; k < S; ++k) {
+                    const float x = (float)u[r][k] / 255.f;
+                    hr[(size_t)r * t + k] = d.hr_norm ? (x - mean) / stdv : x * 2.f - 1.f;
+                }
+            }
+            uint32_t q;
+            if constexpr (S % 2 == 1) {
+                q = u[(S - 1) / 2][(S - 1) / 2];
+            } else {
+                constexpr int c0 = S / 2 - 1;
+                q = (u[c0][c0] + u[c0][c0 + 1] + u[c0 + 1][c0] + u[c0 + 1][c0 + 1] + 2u) >> 2;
+            }
+            d.lr[(plane * lt + ly) * lt + lx] = ((float)q / 255.f - mean) / stdv;
+        }
+    }
+}
+
+int sr_transform_dispatch(const isr_sr_transform_desc* d, hipStream_t s) {
+    const size_t lt = (size_t)(d->t / d->scale), total = (size_t)d->n * lt * lt;
+    const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    switch (d->scale) {
+        case 2: hipLaunchKernelGGL(sr_transform_kernel<2>, dim3(blocks), dim3(256), 0, s, *d); break;
+        case 3: hipLaunchKernelGGL(sr_transform_kernel<3>, dim3(blocks), dim3(256), 0, s, *d); break;
+        case 4: hipLaunchKernelGGL(sr_transform_kernel<4>, dim3(blocks), dim3(256), 0, s, *d); break;
+        default: return -2;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace isr

@@ -83,9 +83,13 @@ class GPUTransform:
         self.scale, self.hr_norm = scale, hr_norm
         self.mean = torch.tensor(mean, device=device).view(1, 3, 1, 1)
         self.std = torch.tensor(std, device=device).view(1, 3, 1, 1)
+        self.mean_f, self.std_f = tuple(float(v) for v in mean), tuple(float(v) for v in std)
         self.device = device
 
     def __call__(self, crops_u8: torch.Tensor):
+        if torch.device(self.device).type == "cuda":
+            return self._hip(crops_u8)
+        # CPU device: the same formulas as torch ops (host-side tests; the GPU path is the kernel)
         x255 = crops_u8.to(self.device, non_blocking=True).float()
         t = x255.shape[-1]
         lr = F.interpolate(x255, size=(t // self.scale, t // self.scale), mode="bilinear", align_corners=False,
@@ -95,6 +99,26 @@ class GPUTransform:
         x = x255.div_(255.0)
         hr = (x - self.mean) / self.std if self.hr_norm else x * 2.0 - 1.0
         return hr.contiguous(), lr.contiguous()
+
+    def _hip(self, crops_u8: torch.Tensor):
+        """One HIP launch (isr_sr_transform): crop block reads, cv2 resize, both Normalizes."""
+        import ctypes
+
+        from . import _lib, ops
+        if crops_u8.dtype != torch.uint8 or crops_u8.dim() != 4 or crops_u8.shape[1] != 3:
+            raise ValueError(f"GPUTransform expects uint8 [n, 3, t, t] crops, got {crops_u8.dtype} "
+                             f"{tuple(crops_u8.shape)}")
+        n, _, t, tw = crops_u8.shape
+        if t != tw or t % self.scale:
+            raise ValueError(f"GPUTransform: square crops with side a multiple of {self.scale}, got {t}x{tw}")
+        x = crops_u8.to(self.device, non_blocking=True).contiguous()
+        hr = torch.empty((n, 3, t, t), device=x.device)
+        lr = torch.empty((n, 3, t // self.scale, t // self.scale), device=x.device)
+        d = _lib.IsrSrTransformDesc(x.data_ptr(), hr.data_ptr(), lr.data_ptr(), n, t, self.scale,
+                                    int(self.hr_norm), (ctypes.c_float * 3)(*self.mean_f),
+                                    (ctypes.c_float * 3)(*self.std_f))
+        _lib.check(_lib.load().isr_sr_transform(ctypes.byref(d), ops._stream()), "isr_sr_transform")
+        return hr, lr
 
 
 class NoisyTransform:

@@ -210,6 +210,21 @@ int isr_pixel_shuffle2(const isr_ew_desc* d, isr_stream_t s);
  * the 2h x 2w grid (rows / cols up to 2ha / 2wa are read); b must be NULL. */
 int isr_pixel_unshuffle2(const isr_ew_desc* d, isr_stream_t s);
 
+/* Training-data transform of SR_dataset (utils/datasets.py:344-355) over a batch of uint8 HR
+ * crops in ONE launch: lr = Normalize(cv2 INTER_LINEAR uint8 resize by `scale`, :302-304: at the
+ * integer factors the block's centre pixel (odd) or its centre 2x2 mean rounded half up (even)),
+ * hr = 2x/255 - 1 (PIL_to_tanh, :96-106) or Normalize(x) when hr_norm (SRGAN mode, :336-339).
+ * crops [n][3][t][t] uint8, hr [n][3][t][t] fp32, lr [n][3][t/scale][t/scale] fp32, all
+ * contiguous; scale in {2, 3, 4}, t % scale == 0; Normalize(v) = (v/255 - mean[c]) / std[c]. */
+typedef struct isr_sr_transform_desc {
+    const uint8_t* crops;
+    float* hr;
+    float* lr;
+    int32_t n, t, scale, hr_norm;
+    float mean[3], std[3];
+} isr_sr_transform_desc;
+int isr_sr_transform(const isr_sr_transform_desc* d, isr_stream_t s);
+
 /* Layout conversion between NCHW fp32 tensors and channel-blocked views
  * (network / loss boundaries: the VGG19 input, utils/loss.py:16-24, and the
  * gradient it receives).  to_blocked writes channels [0, round16(c)) of v (zeros
