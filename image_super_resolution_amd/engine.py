@@ -286,8 +286,11 @@ class ConvChain:
         if grid.t.numel() * 2 >= 2 ** 31:
             raise ValueError("conv chain: activation buffers must stay below 2 GiB (buffer-descriptor window)")
         self.variant = CHAIN_VARIANT if variant is None else variant
-        if self.variant == 3 and grid.ha % 32:
-            raise ValueError("conv chain: variant 3 (32x32 trunk tiles) needs the padded height a multiple of 32")
+        if self.variant in (3, 4) and grid.ha % 32:
+            raise ValueError(f"conv chain: variant {self.variant} (32x32 trunk tiles) needs the padded height "
+                             "a multiple of 32")
+        if self.variant == 4 and any(d.cin % 32 or (d.r1.data and d.cin < 96) for d in descs):
+            raise ValueError("conv chain: variant 4 pairs 16-channel chunks: cin % 32 == 0 (>= 96 with the fold)")
         raw = b"".join(bytes(d) for d in descs)
         self._table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
         self._kinds = torch.tensor(kinds, dtype=torch.int32, device=device)

@@ -384,7 +384,10 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
  * of the per-layer isr_conv3x3_fwd calls bit for bit.  0 = trunk.hip in its two-workgroups-per-CU
  * form (4 waves of 4 output rows each, one K-chunk in flight); 2 = trunk.hip with one 8-wave
  * workgroup per CU (2 output rows per wave) and three chunks in flight; 3 = trunk.hip on 32x32
- * tiles, one 8-wave workgroup per CU (4 rows per wave; needs ha % 32 == 0). */
+ * tiles, one 8-wave workgroup per CU (4 rows per wave; needs ha % 32 == 0); 4 = trunk_deep.hip:
+ * 32x32 tiles, one 8-wave workgroup per CU, split halo (3 slots) / weight (2 slots) rings, the
+ * chunk barrier before the last MFMA step with the next chunk's fragments read behind it, LDS-DMA
+ * spread over the MFMA stream, neighbourhood polls by LDS-DMA (needs ha % 32 == 0). */
 int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
 /* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
  * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,
