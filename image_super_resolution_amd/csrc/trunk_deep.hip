@@ -76,6 +76,7 @@ struct DCtx {
     unsigned gen;
     int nl, G, b, my_tiles;
     uint32_t pstride, abytes;    // bytes per 16-channel plane; bytes of one activation buffer
+    uint32_t hoff[td::HPW];      // per-lane halo piece offsets (chunk-invariant)
     int abl;
 };
 
@@ -88,14 +89,17 @@ __device__ __forceinline__ const_geo& geo_of(const DCtx& c) {
 __device__ __forceinline__ int cL(uint32_t p) { return (int)(p >> 21); }
 __device__ __forceinline__ int cK(uint32_t p) { return (int)((p >> 8) & 8191); }
 __device__ __forceinline__ int cCH(uint32_t p) { return (int)(p & 255); }
-__device__ __forceinline__ int lay_nch(const DCtx& c, int L) { return rec_nch(c.recs[L]); }
-__device__ __forceinline__ int lay_wpc(const DCtx& c, int L) { return rec_kind(c.recs[L]) == 0 ? tk::WPG : tk::WPF; }
+// A cursor may stand past the stream's last layer (it stops there); the branch-free staging code
+// still reads its layer's record, so record reads clamp to the last layer (nl may be 1024, the
+// records' capacity).
+__device__ __forceinline__ const_rec& rec_at(const DCtx& c, int L) { return c.recs[L < c.nl ? L : c.nl - 1]; }
+__device__ __forceinline__ int lay_nch(const DCtx& c, int L) { return rec_nch(rec_at(c, L)); }
+__device__ __forceinline__ int lay_wpc(const DCtx& c, int L) { return rec_kind(rec_at(c, L)) == 0 ? tk::WPG : tk::WPF; }
 
 __device__ __forceinline__ uint32_t cur_next(const DCtx& c, uint32_t p) {
     const int L = cL(p), k = cK(p);
-    if (cCH(p) + 1 < lay_nch(c, L)) return p + 1;
-    if (k + 1 < c.my_tiles) return (uint32_t)L << 21 | (uint32_t)(k + 1) << 8;
-    return (uint32_t)(L + 1) << 21;
+    const uint32_t next_tile = k + 1 < c.my_tiles ? ((uint32_t)L << 21 | (uint32_t)(k + 1) << 8) : (uint32_t)(L + 1) << 21;
+    return cCH(p) + 1 < lay_nch(c, L) ? p + 1 : next_tile;  // (selects: no branch in the MFMA stream)
 }
 
 // bias slot of the cursor's tile: the workgroup's tile sequence number & 3
@@ -108,7 +112,7 @@ __device__ __forceinline__ int cur_bslot(const DCtx& c, uint32_t p) { return (cL
 __device__ __forceinline__ bool cur_needs_dep(const DCtx& c, uint32_t p) {
     const int L = cL(p);
     if (L == 0) return false;
-    const int fnew = rec_first_new(c.recs[L]);
+    const int fnew = rec_first_new(rec_at(c, L));
     return fnew != tk::NEED_NONE && (cCH(p) >= fnew || fnew >= lay_nch(c, L));
 }
 
@@ -169,7 +173,7 @@ __device__ __forceinline__ uint32_t get_mark(const DStream& s, int j) {
 
 // halo source offset of the cursor's item, from the tile table's base `hb`
 __device__ __forceinline__ uint32_t halo_src(const DCtx& c, uint32_t p, uint32_t hb) {
-    return hb + (uint32_t)(rec_xp(c.recs[cL(p)]) + cCH(p)) * c.pstride;
+    return hb + (uint32_t)(rec_xp(rec_at(c, cL(p))) + cCH(p)) * c.pstride;
 }
 
 // ---- staging pieces.  Branch-free inside the MFMA stream: every call issues exactly one
@@ -184,22 +188,22 @@ __device__ __forceinline__ void stage_h_piece(const DCtx& c, DStream& s) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int j = wave_id() + td::WM * K;
     const bool on = has(s, F_GO_H) && j < td::HP && !(c.abl & 1);
-    const_rec& r = c.recs[cL(s.hcur)];
+    const_rec& r = rec_at(c, cL(s.hcur));
     char* dst = on ? smem + (s.hi % td::NSH) * td::HSLOT + j * 1024 : smem + td::DUMMY_OFF;
-    // this lane's halo unit (recomputed: a per-piece register array cost 5 VGPRs the MFMA loop lacks)
-    const uint32_t hoff = halo_piece_off<td::HQ>(j, threadIdx.x & 63, geo_of(c).wp);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n((const void*)(uintptr_t)r.x, c.abytes), ISR_LDS_PTR(dst), 16,
-                                             hoff, on ? s.hso : OOR, 0, 16);
+                                             c.hoff[K], on ? s.hso : OOR, 0, 16);
     ++s.issued;
 }
 
 __device__ __forceinline__ void finish_h(const DCtx& c, DStream& s) {
-    if (!has(s, F_GO_H)) return;
-    set_mark(s, s.hi, s.issued);
-    ++s.hi;
+    const bool go = has(s, F_GO_H);
     const uint32_t nx = cur_next(c, s.hcur);
-    if ((nx >> 8) != (s.hcur >> 8)) setf(s, F_HDEP, false);  // a new tile: not confirmed yet
-    s.hcur = nx;
+    const uint32_t m = get_mark(s, s.hi);
+    set_mark(s, s.hi, go ? s.issued : m);
+    const bool newtile = go && (nx >> 8) != (s.hcur >> 8);  // a new tile: not confirmed yet
+    s.fl = newtile ? (s.fl & ~F_HDEP) : s.fl;
+    s.hcur = go ? nx : s.hcur;
+    s.hi += go ? 1 : 0;
     setf(s, F_GO_H, false);
 }
 
@@ -209,7 +213,7 @@ __device__ __forceinline__ void stage_w_piece(const DCtx& c, DStream& s) {
     const int lane = threadIdx.x & 63, j = wave_id() + td::WM * K;
     const int L = cL(s.wcur), wpc = lay_wpc(c, L);
     const bool on = has(s, F_GO_W) && j < wpc && !(c.abl & 8);
-    const_rec& r = c.recs[L];
+    const_rec& r = rec_at(c, L);
     const uint32_t wbytes = (uint32_t)(rec_nch(r) * wpc * 1024);
     char* dst = on ? smem + td::W_OFF + (s.wi & 1) * td::WSLOT + j * 1024 : smem + td::DUMMY_OFF;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n((const void*)(uintptr_t)r.w, wbytes), ISR_LDS_PTR(dst), 16,
@@ -223,7 +227,7 @@ __device__ __forceinline__ void stage_bias(const DCtx& c, DStream& s) {
     const int L = cL(s.wcur);
     const bool on = has(s, F_GO_W) && cCH(s.wcur) == 0 && wave_id() == 0;
     const int lane = threadIdx.x & 63, cout = lay_wpc(c, L) == tk::WPG ? 32 : 64;
-    const_rec& r = c.recs[L];
+    const_rec& r = rec_at(c, L);
     char* dst = on ? smem + td::BIAS_OFF + cur_bslot(c, s.wcur) * 256 : smem + td::DUMMY_OFF;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n((const void*)(uintptr_t)r.b, (uint32_t)cout * 4),
                                              ISR_LDS_PTR(dst), 4, lane * 4, on ? 0u : OOR, 0, 0);
@@ -231,10 +235,11 @@ __device__ __forceinline__ void stage_bias(const DCtx& c, DStream& s) {
 }
 
 __device__ __forceinline__ void finish_w(const DCtx& c, DStream& s) {
-    if (!has(s, F_GO_W)) return;
-    set_mark(s, s.wi, s.issued);
-    ++s.wi;
-    s.wcur = cur_next(c, s.wcur);
+    const bool go = has(s, F_GO_W);
+    const uint32_t m = get_mark(s, s.wi);
+    set_mark(s, s.wi, go ? s.issued : m);
+    s.wcur = go ? cur_next(c, s.wcur) : s.wcur;
+    s.wi += go ? 1 : 0;
     setf(s, F_GO_W, false);
 }
 
@@ -248,11 +253,9 @@ __device__ __forceinline__ void stage_poll(const DCtx& c, DStream& s, int nb) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(c.state, (uint32_t)(4 + geo_of(c).ntiles) * 4), ISR_LDS_PTR(dst),
                                              4, nb >= 0 ? (uint32_t)(4 + nb) * 4 : OOR, on ? 0u : OOR, 0, 16);
     ++s.issued;
-    if (go) {
-        setf(s, F_POLL, true);
-        setf(s, F_POLLP, (s.i & 1) != 0);
-        s.poll_mark = s.issued;
-    }
+    const uint32_t pf = F_POLL | ((s.i & 1) ? F_POLLP : 0u);
+    s.fl = go ? ((s.fl & ~(F_POLL | F_POLLP)) | pf) : s.fl;
+    s.poll_mark = go ? s.issued : s.poll_mark;
     setf(s, F_GO_POLL, false);
 }
 
@@ -327,9 +330,14 @@ __device__ __forceinline__ void d_slow_path(const DCtx& c, DStream& s) {
 
 // The chunk barrier of item i (before its dx = 2 step): every wave's reads of item i's slots are
 // done (lgkmcnt(0) in raw_barrier), its own pieces of item i+1 (and the pending tile's stores,
-// and an outstanding poll) have landed.  After it: publish, read the poll, decide the staging of
-// the next period (weights of i+2, halo of up to i+3).  Returns this lane's neighbour of the halo
-// cursor's tile (for a poll to issue).
+// and an outstanding poll) have landed.  After it: publish, read the poll, and, when item i+1
+// continues this tile (MORE: its step-0 fragments are read right behind this barrier) but was
+// not staged, stage it now — blocking on the neighbourhood if needed; safe mid-tile: the wait is
+// for layer L-1 of the neighbours, never for this workgroup's unfinished tile, and its previous
+// tile was just published — then a second barrier.  Last, decide the next period's staging
+// (weights of i+2, halo of up to i+3).  Returns this lane's neighbour of the halo cursor's tile
+// (for a poll to issue).
+template <bool MORE>
 __device__ __forceinline__ int d_barrier(const DCtx& c, DStream& s) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int i = s.i;
@@ -345,33 +353,43 @@ __device__ __forceinline__ int d_barrier(const DCtx& c, DStream& s) {
     if (has(s, F_POLL)) want(s.poll_mark);
     if (any) wait_vm(s.issued - tgt);
     // the halo cursor's tile: read before the barrier (its lgkmcnt(0) covers the reads)
-    const int hk = cK(s.hcur);
-    const uint32_t hb = tbl_hbase(hk), hpos = tbl_pos(hk);
+    int hk = cK(s.hcur);
+    uint32_t hb = tbl_hbase(hk), hpos = tbl_pos(hk);
     raw_barrier();
     setf(s, F_READY, next_staged);
     if (s.pend >= 0) d_publish(c, s);
-    const int nb = nb_of_pos(c, hpos);
+    int nb = nb_of_pos(c, hpos);
     // the poll issued at an earlier barrier has landed in its slot: the neighbourhood's verdict
-    bool poll_ok = false;
     if (has(s, F_POLL)) {
         const int lane = threadIdx.x & 63;
         const unsigned v = *reinterpret_cast<const volatile unsigned*>(smem + td::POLL_OFF +
                                                                        (has(s, F_POLLP) ? 256 : 0) + lane * 4);
         const unsigned need = c.gen * 1024u + (unsigned)cL(s.hcur);  // done with layer L - 1
-        poll_ok = __all(nb < 0 || (int)(v - need) >= 0);
+        if (__all(nb < 0 || (int)(v - need) >= 0)) setf(s, F_HDEP, true);
         setf(s, F_POLL, false);
+    }
+    if (MORE && !next_staged) {
+        if (s.wi <= i + 1) stage_w_block(c, s);
+        if (s.hi <= i + 1) {
+            if (cur_needs_dep(c, s.hcur) && !has(s, F_HDEP)) {
+                if (!(c.abl & 16)) dep_wait(c.state, nb, c.gen * 1024u + (unsigned)cL(s.hcur), c.gen);
+                setf(s, F_HDEP, true);
+            }
+            stage_h_block(c, s);
+        }
+        wait_vm(s.issued - get_mark(s, i + 1));
+        raw_barrier();
+        setf(s, F_READY, true);
+        hk = cK(s.hcur);
+        hb = __builtin_amdgcn_readfirstlane(tbl_hbase(hk));
+        nb = nb_of_pos(c, tbl_pos(hk));
     }
     // weights of the next unstaged item (normally i+2; its slot held item i, free now)
     setf(s, F_GO_W, s.wi <= i + 2 && cL(s.wcur) < c.nl);
     // halo of the next unstaged item up to i+3 (its slot held item hi-3 <= i)
     setf(s, F_GO_H, false);
     if (s.hi <= i + 3 && cL(s.hcur) < c.nl) {
-        bool go = !cur_needs_dep(c, s.hcur) || has(s, F_HDEP) || (c.abl & 16);
-        if (!go && poll_ok) {
-            setf(s, F_HDEP, true);
-            go = true;
-        }
-        if (go) {
+        if (!cur_needs_dep(c, s.hcur) || has(s, F_HDEP) || (c.abl & 16)) {
             setf(s, F_GO_H, true);
             s.hso = halo_src(c, s.hcur, __builtin_amdgcn_readfirstlane(hb));
         } else {
@@ -441,16 +459,16 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
     // The residual fold of chunks 0..3 (couts 16 ch .. + 16: fragment ch >> 1, half P) adds its
     // 4 MFMAs after step 1's dy = 1 rows, i.e. between each accumulator's dy = 1 and dy = 2
     // contributions of dx = 1 — the same point of the same order as conv3x3.hip.
-    auto chunk = [&](const int ch, auto p_tag, auto more_tag, auto fold_tag) {
+    auto chunk = [&](const int ch, auto p_tag, auto more_tag, auto fold_tag, auto first_tag) {
         constexpr int P = decltype(p_tag)::value;
-        constexpr bool MORE = decltype(more_tag)::value != 0;  // the next item continues this tile
-        constexpr int FF = decltype(fold_tag)::value;  // fold target fragment (chunks 0..3), or -1
+        constexpr bool MORE = decltype(more_tag)::value != 0;    // the next item continues this tile
+        constexpr int FF = decltype(fold_tag)::value;            // fold target fragment (chunks 0..3), or -1
+        constexpr bool FIRST = decltype(first_tag)::value != 0;  // the tile's chunk 0: nothing prefetched
         const int it = s.i;
-        if (!has(s, F_FRAGS)) {
+        if constexpr (FIRST) {
             if (!has(s, F_READY)) d_slow_path(c, s);
             read_step0(it, P);
         }
-        setf(s, F_FRAGS, false);
         setf(s, F_READY, false);
         int pnb = -1;
         if (ch == 0) {
@@ -475,7 +493,7 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
             const int cur = (P + stp) & 1;
             if (stp == 2) {
                 __builtin_amdgcn_s_setprio(0);
-                pnb = d_barrier(c, s);
+                pnb = d_barrier<MORE>(c, s);
                 __builtin_amdgcn_s_setprio(1);
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -488,7 +506,7 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
                     // input row ia = r + dyi is last used here when dyi == min(2, ia)
                     if (dyi == 2 || r == 0) {
                         if (stp < 2) read_one(it, stp + 1, TN * NF + r + dyi, cur ^ 1);
-                        else if (MORE) read_one(it + 1, 0, TN * NF + r + dyi, cur ^ 1);  // (re-read if not ready)
+                        else if (MORE) read_one(it + 1, 0, TN * NF + r + dyi, cur ^ 1);
                     }
                     // spread staging
                     const int q = dyi * R + r;
@@ -534,28 +552,38 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
             }
         }
         __builtin_amdgcn_s_setprio(0);
-        setf(s, F_FRAGS, MORE && has(s, F_READY));
         ++s.i;
     };
 
-    // chunks 0..3 of a folding final conv carry the residual fold (nch >= 12 there)
-    int ch0 = 0;
+    // chunk sequence: chunk 0 reads its step-0 fragments at the top (nothing is prefetched across
+    // tiles), every later chunk gets them from the previous chunk's dx = 2 step; the register set
+    // alternates (P = ch & 1, nch even).  A final conv (NF = 2) always folds (variant 4 needs it):
+    // chunks 0..3 carry the residual fold.
+    using T0 = PIC<0>;
+    using T1 = PIC<1>;
+    using TN1 = PIC<-1>;
     if constexpr (NF == 2) {
-        if (fold) {
-            chunk(0, PIC<0>{}, PIC<1>{}, PIC<0>{});
-            chunk(1, PIC<1>{}, PIC<1>{}, PIC<0>{});
-            chunk(2, PIC<0>{}, PIC<1>{}, PIC<1>{});
-            chunk(3, PIC<1>{}, PIC<1>{}, PIC<1>{});
-            ch0 = 4;
-        }
-    }
+        chunk(0, T0{}, T1{}, T0{}, T1{});
+        chunk(1, T1{}, T1{}, T0{}, T0{});
+        chunk(2, T0{}, T1{}, T1{}, T0{});
+        chunk(3, T1{}, T1{}, T1{}, T0{});
 #pragma nounroll
-    for (int ch = ch0; ch < nch - 2; ch += 2) {
-        chunk(ch, PIC<0>{}, PIC<1>{}, PIC<-1>{});
-        chunk(ch + 1, PIC<1>{}, PIC<1>{}, PIC<-1>{});
+        for (int ch = 4; ch < nch - 2; ch += 2) {
+            chunk(ch, T0{}, T1{}, TN1{}, T0{});
+            chunk(ch + 1, T1{}, T1{}, TN1{}, T0{});
+        }
+        chunk(nch - 2, T0{}, T1{}, TN1{}, T0{});
+        chunk(nch - 1, T1{}, T0{}, TN1{}, T0{});
+    } else {
+        chunk(0, T0{}, T1{}, TN1{}, T1{});
+#pragma nounroll
+        for (int ch = 1; ch < nch - 1; ch += 2) {
+            chunk(ch, T1{}, T1{}, TN1{}, T0{});
+            chunk(ch + 1, T0{}, T1{}, TN1{}, T0{});
+        }
+        chunk(nch - 1, T1{}, T0{}, TN1{}, T0{});
     }
-    chunk(nch - 2, PIC<0>{}, PIC<1>{}, PIC<-1>{});
-    chunk(nch - 1, PIC<1>{}, PIC<0>{}, PIC<-1>{});
+    (void)fold;
 
     // ---- epilogue: straight from the accumulators, write-through (sc1) stores ----
     {
@@ -645,12 +673,13 @@ __global__ __launch_bounds__(td::NT, 2) void trunk_deep_kernel(unsigned* state, 
         }
         return;
     }
-    // this form pairs chunks (register sets alternate) and peels the 4 fold chunks ahead of at
-    // least one more pair: every layer needs an even chunk count, a folding one at least 6
+    // this form pairs chunks (register sets alternate) and peels a final conv's 4 fold chunks
+    // ahead of at least one more pair: every layer needs an even chunk count; a final conv the
+    // residual fold and at least 6 chunks
     bool shape_ok = true;
     for (int L = 0; L < nl; ++L) {
         const int n = rec_nch(c.recs[L]);
-        shape_ok = shape_ok && (n % 2 == 0) && n >= 2 && (!rec_fold(c.recs[L]) || n >= 6);
+        shape_ok = shape_ok && (n % 2 == 0) && n >= 2 && (rec_kind(c.recs[L]) == 0 || (rec_fold(c.recs[L]) && n >= 6));
     }
     if (!shape_ok) {
         if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -667,6 +696,11 @@ __global__ __launch_bounds__(td::NT, 2) void trunk_deep_kernel(unsigned* state, 
     c.pstride = (uint32_t)(g.hp * g.wp * 32);
     c.abytes = (uint32_t)((size_t)g.n * g.cs16 * c.pstride);  // < 2 GiB (prep err bit 64)
     c.abl = trunkd_abl();
+    {
+        const int wave = wave_id(), lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < td::HPW; ++k) c.hoff[k] = halo_piece_off<td::HQ>(wave + td::WM * k, lane, g.wp);
+    }
     // the tile table (launcher: my_tiles <= MAX_TILES)
     {
         extern __shared__ __attribute__((aligned(16))) char smem[];

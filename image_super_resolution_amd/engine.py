@@ -289,8 +289,10 @@ class ConvChain:
         if self.variant in (3, 4) and grid.ha % 32:
             raise ValueError(f"conv chain: variant {self.variant} (32x32 trunk tiles) needs the padded height "
                              "a multiple of 32")
-        if self.variant == 4 and any(d.cin % 32 or (d.r1.data and d.cin < 96) for d in descs):
-            raise ValueError("conv chain: variant 4 pairs 16-channel chunks: cin % 32 == 0 (>= 96 with the fold)")
+        if self.variant == 4 and any(d.cin % 32 or (k == 1 and (not d.r1.data or d.cin < 96))
+                                     for d, k in zip(descs, kinds)):
+            raise ValueError("conv chain: variant 4 pairs 16-channel chunks (cin % 32 == 0) and needs every "
+                             "64-cout layer to fold its residual r1 (cin >= 96)")
         raw = b"".join(bytes(d) for d in descs)
         self._table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
         self._kinds = torch.tensor(kinds, dtype=torch.int32, device=device)
