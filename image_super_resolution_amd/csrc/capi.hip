@@ -19,6 +19,7 @@ size_t trunk_state_words(int n, int ha, int wa);
 int trunk_launch(const isr_chain_desc* c, hipStream_t s, int form);
 int trunk_stamps_set(void* p);
 int trunk_knobs_set(const int* k);
+int trunk_deep_stats(unsigned long long* out, int reset);
 int trunk_item_stamps_set(void* p);
 size_t conv3x3_packed_bytes(int cout, int cin);
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
@@ -264,6 +265,12 @@ int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k
     const int rc = isr::trunk_knobs_set(k);
     if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "trunk knobs: library built without -DISR_TUNING");
     return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "trunk knobs: hipMemcpyToSymbol failed");
+}
+
+int isr_tuning_trunk_deep_stats(uint64_t* out, int32_t reset) {
+    const int rc = isr::trunk_deep_stats((unsigned long long*)out, reset);
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "trunk deep stats: library built without -DISR_TUNING");
+    return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "trunk deep stats: hipMemcpyFromSymbol failed");
 }
 
 int isr_tuning_trunk_item_stamps(void* buf) {

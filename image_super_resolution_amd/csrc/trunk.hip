@@ -912,7 +912,9 @@ int trunk_knobs_set(const int* k) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
 }
 int trunk_stamps_set(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
+int trunk_deep_stamps_set(void* p);  // trunk_deep.hip (the same buffer layout)
 int trunk_item_stamps_set(void* p) {
+    if (trunk_deep_stamps_set(p) != 0) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_item_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
 }
 #else

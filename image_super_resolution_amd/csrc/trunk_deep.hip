@@ -57,9 +57,30 @@ static_assert(HQ / 34 == TH + 2 && tk::HC == HC, "halo image geometry shared wit
 
 #ifdef ISR_TUNING
 __device__ int g_trunkd_knobs[4];
+// event counters (tuning builds): [0] top slow paths, [1] their blocking waits, [2] mid-chunk slow
+// paths, [3] their blocking waits, [4] polls issued, [5] polls that found the neighbourhood done
+__device__ unsigned long long g_trunkd_stats[8];
 __device__ __forceinline__ int trunkd_abl() { return __builtin_amdgcn_readfirstlane(g_trunkd_knobs[0]); }
+__device__ __forceinline__ void trunkd_count(int k) {
+    if (threadIdx.x == 0) atomicAdd(&g_trunkd_stats[k], 1ull);
+}
+// per-chunk cycle stamps (s_memtime) of layers 77 (growth2) and 79 (final), each workgroup's first
+// tile, lane 0 of waves 0 and 4: [grid][2][16 chunks][2][8]: [0] chunk top, [1] step-0 fragments
+// requested, [2] steps 0-1 issued, [3] own DMA waited, [4] barrier passed, [5] decisions done,
+// [6] step 2 issued
+__device__ unsigned long long* g_trunkd_stamps;
+__device__ __forceinline__ void trunkd_stamp(int L, int k, int ch, int slot) {
+    unsigned long long* p = g_trunkd_stamps;
+    const int w = wave_id();
+    if (p != nullptr && k == 0 && (threadIdx.x & 63) == 0 && (w == 0 || w == 4) && (L == 77 || L == 79) && ch < 16) {
+        const unsigned long long v = __builtin_amdgcn_s_memtime();
+        p[((((size_t)blockIdx.x * 2 + (L == 79)) * 16 + ch) * 2 + (w != 0)) * 8 + slot] = v;
+    }
+}
 #else
 __device__ __forceinline__ int trunkd_abl() { return 0; }
+__device__ __forceinline__ void trunkd_count(int) {}
+__device__ __forceinline__ void trunkd_stamp(int, int, int, int) {}
 #endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_n(const void* p, uint32_t bytes) {
@@ -75,6 +96,7 @@ struct DCtx {
     const_rec* recs;
     unsigned gen;
     int nl, G, b, my_tiles;
+    uint32_t nbxy;               // tiles per row | per column << 16
     uint32_t pstride, abytes;    // bytes per 16-channel plane; bytes of one activation buffer
     uint32_t hoff[td::HPW];      // per-lane halo piece offsets (chunk-invariant)
     int abl;
@@ -93,13 +115,31 @@ __device__ __forceinline__ int cCH(uint32_t p) { return (int)(p & 255); }
 // still reads its layer's record, so record reads clamp to the last layer (nl may be 1024, the
 // records' capacity).
 __device__ __forceinline__ const_rec& rec_at(const DCtx& c, int L) { return c.recs[L < c.nl ? L : c.nl - 1]; }
-__device__ __forceinline__ int lay_nch(const DCtx& c, int L) { return rec_nch(rec_at(c, L)); }
-__device__ __forceinline__ int lay_wpc(const DCtx& c, int L) { return rec_kind(rec_at(c, L)) == 0 ? tk::WPG : tk::WPF; }
 
-__device__ __forceinline__ uint32_t cur_next(const DCtx& c, uint32_t p) {
+// A cursor's layer in one word (kept beside the cursor, re-read from the record only when the
+// cursor changes layer — record loads on the barrier's critical path cost ~1,000 cycles per chunk):
+// nch | first_new << 8 | xp << 16 | wpc << 24.
+__device__ __forceinline__ uint32_t lay_info(const DCtx& c, int L) {
+    const_rec& r = rec_at(c, L);
+    return (uint32_t)rec_nch(r) | (uint32_t)rec_first_new(r) << 8 | (uint32_t)rec_xp(r) << 16 |
+           (uint32_t)(rec_kind(r) == 0 ? tk::WPG : tk::WPF) << 24;
+}
+__device__ __forceinline__ int inf_nch(uint32_t f) { return (int)(f & 255); }
+__device__ __forceinline__ int inf_fnew(uint32_t f) { return (int)((f >> 8) & 255); }
+__device__ __forceinline__ int inf_xp(uint32_t f) { return (int)((f >> 16) & 255); }
+__device__ __forceinline__ int inf_wpc(uint32_t f) { return (int)(f >> 24); }
+
+// advance cursor p (layer info f) by one item; a layer change re-reads f
+__device__ __forceinline__ void cur_adv(const DCtx& c, uint32_t& p, uint32_t& f) {
     const int L = cL(p), k = cK(p);
-    const uint32_t next_tile = k + 1 < c.my_tiles ? ((uint32_t)L << 21 | (uint32_t)(k + 1) << 8) : (uint32_t)(L + 1) << 21;
-    return cCH(p) + 1 < lay_nch(c, L) ? p + 1 : next_tile;  // (selects: no branch in the MFMA stream)
+    if (cCH(p) + 1 < inf_nch(f)) {
+        ++p;
+    } else if (k + 1 < c.my_tiles) {
+        p = (uint32_t)L << 21 | (uint32_t)(k + 1) << 8;
+    } else {
+        p = (uint32_t)(L + 1) << 21;
+        f = lay_info(c, L + 1);
+    }
 }
 
 // bias slot of the cursor's tile: the workgroup's tile sequence number & 3
@@ -109,11 +149,10 @@ __device__ __forceinline__ int cur_bslot(const DCtx& c, uint32_t p) { return (cL
 // chunks from the first one layer L-1 wrote; every chunk of a layer that reads nothing its
 // predecessor wrote (so that every tile of layer >= 1 confirms its neighbourhood before its
 // stores land, and the next layer's older chunks are final when its cursor gets there).
-__device__ __forceinline__ bool cur_needs_dep(const DCtx& c, uint32_t p) {
-    const int L = cL(p);
-    if (L == 0) return false;
-    const int fnew = rec_first_new(rec_at(c, L));
-    return fnew != tk::NEED_NONE && (cCH(p) >= fnew || fnew >= lay_nch(c, L));
+__device__ __forceinline__ bool cur_needs_dep(uint32_t p, uint32_t f) {
+    if (cL(p) == 0) return false;
+    const int fnew = inf_fnew(f);
+    return fnew != tk::NEED_NONE && (cCH(p) >= fnew || fnew >= inf_nch(f));
 }
 
 __device__ __forceinline__ uint32_t tbl_hbase(int k) {
@@ -130,7 +169,7 @@ __device__ __forceinline__ int nb_of_pos(const DCtx& c, uint32_t pos) {
     const int lane = threadIdx.x & 63;
     const int img = (int)(pos & 1023), by = (int)((pos >> 10) & 2047), bx = (int)(pos >> 21);
     const int yy = by + lane / 3 - 1, xx = bx + lane % 3 - 1;
-    const int nbx = geo_of(c).nbx, nby = geo_of(c).nby;
+    const int nbx = (int)(c.nbxy & 0xffff), nby = (int)(c.nbxy >> 16);
     return (lane < 9 && yy >= 0 && yy < nby && xx >= 0 && xx < nbx) ? (img * nby + yy) * nbx + xx : -1;
 }
 
@@ -139,11 +178,13 @@ struct DStream {
     int i;                 // item being computed
     int wi, hi;            // next item whose weights / halo are not staged yet
     uint32_t wcur, hcur;   // their positions
+    uint32_t winf, hinf;   // their layers' info words (lay_info)
     uint32_t hso;          // halo source offset of item hi (set with F_GO_H)
     uint32_t fl;           // flags (F_*), packed: wave-uniform bools would take an SGPR pair each
     uint32_t issued;       // vector-memory instructions issued by this wave
     uint32_t mk0, mk1, mk2, mk3;  // mark of item j (at j & 3): `issued` after its last piece
     uint32_t poll_mark;    // `issued` after the outstanding poll (F_POLL)
+    uint32_t poll_tile;    // its tile (the cursor's L, k: hcur >> 8 when it was issued)
     int pend;              // the finished tile whose progress word waits for its stores:
                            // t << 11 | (L + 1), or -1
     uint32_t pend_mark;
@@ -172,38 +213,30 @@ __device__ __forceinline__ uint32_t get_mark(const DStream& s, int j) {
 }
 
 // halo source offset of the cursor's item, from the tile table's base `hb`
-__device__ __forceinline__ uint32_t halo_src(const DCtx& c, uint32_t p, uint32_t hb) {
-    return hb + (uint32_t)(rec_xp(rec_at(c, cL(p))) + cCH(p)) * c.pstride;
+__device__ __forceinline__ uint32_t halo_src(const DCtx& c, uint32_t p, uint32_t f, uint32_t hb) {
+    return hb + (uint32_t)(inf_xp(f) + cCH(p)) * c.pstride;
 }
 
-// ---- staging pieces.  Branch-free inside the MFMA stream: every call issues exactly one
-// LDS-DMA instruction per wave; an inactive one (nothing to stage, or not this wave's piece) reads
-// out of its buffer's range — zeros — into a dummy LDS area.  So each position's vmcnt count is
-// static and no basic block splits the MFMA schedule (a branchy form pushed the main loop past
-// 256 VGPRs). ----
-constexpr uint32_t OOR = 0x7ffffff0u;  // a source offset beyond every buffer's range
-
+// ---- staging pieces: one LDS-DMA instruction each when active (wave-uniform branch) ----
 template <int K>
 __device__ __forceinline__ void stage_h_piece(const DCtx& c, DStream& s) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int j = wave_id() + td::WM * K;
-    const bool on = has(s, F_GO_H) && j < td::HP && !(c.abl & 1);
+    if (!has(s, F_GO_H) || j >= td::HP || (c.abl & 1)) return;
     const_rec& r = rec_at(c, cL(s.hcur));
-    char* dst = on ? smem + (s.hi % td::NSH) * td::HSLOT + j * 1024 : smem + td::DUMMY_OFF;
+    char* dst = smem + (s.hi % td::NSH) * td::HSLOT + j * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n((const void*)(uintptr_t)r.x, c.abytes), ISR_LDS_PTR(dst), 16,
-                                             c.hoff[K], on ? s.hso : OOR, 0, 16);
+                                             c.hoff[K], s.hso, 0, 16);
     ++s.issued;
 }
 
 __device__ __forceinline__ void finish_h(const DCtx& c, DStream& s) {
-    const bool go = has(s, F_GO_H);
-    const uint32_t nx = cur_next(c, s.hcur);
-    const uint32_t m = get_mark(s, s.hi);
-    set_mark(s, s.hi, go ? s.issued : m);
-    const bool newtile = go && (nx >> 8) != (s.hcur >> 8);  // a new tile: not confirmed yet
-    s.fl = newtile ? (s.fl & ~F_HDEP) : s.fl;
-    s.hcur = go ? nx : s.hcur;
-    s.hi += go ? 1 : 0;
+    if (!has(s, F_GO_H)) return;
+    set_mark(s, s.hi, s.issued);
+    ++s.hi;
+    const uint32_t old = s.hcur;
+    cur_adv(c, s.hcur, s.hinf);
+    if ((s.hcur >> 8) != (old >> 8)) setf(s, F_HDEP, false);  // a new tile: not confirmed yet
     setf(s, F_GO_H, false);
 }
 
@@ -211,58 +244,61 @@ template <int K>
 __device__ __forceinline__ void stage_w_piece(const DCtx& c, DStream& s) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, j = wave_id() + td::WM * K;
-    const int L = cL(s.wcur), wpc = lay_wpc(c, L);
-    const bool on = has(s, F_GO_W) && j < wpc && !(c.abl & 8);
+    const int L = cL(s.wcur), wpc = inf_wpc(s.winf);
+    if (!has(s, F_GO_W) || j >= wpc || (c.abl & 8)) return;
     const_rec& r = rec_at(c, L);
-    const uint32_t wbytes = (uint32_t)(rec_nch(r) * wpc * 1024);
-    char* dst = on ? smem + td::W_OFF + (s.wi & 1) * td::WSLOT + j * 1024 : smem + td::DUMMY_OFF;
+    const uint32_t wbytes = (uint32_t)(inf_nch(s.winf) * wpc * 1024);
+    char* dst = smem + td::W_OFF + (s.wi & 1) * td::WSLOT + j * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n((const void*)(uintptr_t)r.w, wbytes), ISR_LDS_PTR(dst), 16,
-                                             lane * 16, on ? (uint32_t)(cCH(s.wcur) * wpc + j) * 1024 : OOR, 0, 0);
+                                             lane * 16, (uint32_t)(cCH(s.wcur) * wpc + j) * 1024, 0, 0);
     ++s.issued;
 }
 
 // the bias of a tile's first chunk (wave 0: 4 B per lane; lanes beyond cout read zeros)
 __device__ __forceinline__ void stage_bias(const DCtx& c, DStream& s) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (!has(s, F_GO_W) || cCH(s.wcur) != 0 || wave_id() != 0) return;
     const int L = cL(s.wcur);
-    const bool on = has(s, F_GO_W) && cCH(s.wcur) == 0 && wave_id() == 0;
-    const int lane = threadIdx.x & 63, cout = lay_wpc(c, L) == tk::WPG ? 32 : 64;
+    const int lane = threadIdx.x & 63, cout = inf_wpc(s.winf) == tk::WPG ? 32 : 64;
     const_rec& r = rec_at(c, L);
-    char* dst = on ? smem + td::BIAS_OFF + cur_bslot(c, s.wcur) * 256 : smem + td::DUMMY_OFF;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n((const void*)(uintptr_t)r.b, (uint32_t)cout * 4),
-                                             ISR_LDS_PTR(dst), 4, lane * 4, on ? 0u : OOR, 0, 0);
+                                             ISR_LDS_PTR(smem + td::BIAS_OFF + cur_bslot(c, s.wcur) * 256), 4,
+                                             lane * 4, 0, 0, 0);
     ++s.issued;
 }
 
 __device__ __forceinline__ void finish_w(const DCtx& c, DStream& s) {
-    const bool go = has(s, F_GO_W);
-    const uint32_t m = get_mark(s, s.wi);
-    set_mark(s, s.wi, go ? s.issued : m);
-    s.wcur = go ? cur_next(c, s.wcur) : s.wcur;
-    s.wi += go ? 1 : 0;
+    if (!has(s, F_GO_W)) return;
+    set_mark(s, s.wi, s.issued);
+    ++s.wi;
+    cur_adv(c, s.wcur, s.winf);
     setf(s, F_GO_W, false);
 }
 
 // the neighbourhood poll of the halo cursor's tile (this lane's neighbour nb, from d_barrier):
 // 9 progress words (sc1) into poll slot (item & 1) by wave 0; read by every wave after the
-// barrier that follows its vmcnt wait (lanes without a neighbour write zeros, never read)
+// barrier that follows its vmcnt wait
 __device__ __forceinline__ void stage_poll(const DCtx& c, DStream& s, int nb) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const bool go = has(s, F_GO_POLL), on = go && wave_id() == 0;
-    char* dst = on ? smem + td::POLL_OFF + (s.i & 1) * 256 : smem + td::DUMMY_OFF;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(c.state, (uint32_t)(4 + geo_of(c).ntiles) * 4), ISR_LDS_PTR(dst),
-                                             4, nb >= 0 ? (uint32_t)(4 + nb) * 4 : OOR, on ? 0u : OOR, 0, 16);
-    ++s.issued;
-    const uint32_t pf = F_POLL | ((s.i & 1) ? F_POLLP : 0u);
-    s.fl = go ? ((s.fl & ~(F_POLL | F_POLLP)) | pf) : s.fl;
-    s.poll_mark = go ? s.issued : s.poll_mark;
+    if (!has(s, F_GO_POLL)) return;
+    if (wave_id() == 0) {
+        if (nb >= 0)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(c.state, (uint32_t)(4 + geo_of(c).ntiles) * 4),
+                                                     ISR_LDS_PTR(smem + td::POLL_OFF + (s.i & 1) * 256), 4,
+                                                     (uint32_t)(4 + nb) * 4, 0, 0, 16);
+        ++s.issued;
+    }
+    setf(s, F_POLL, true);
+    setf(s, F_POLLP, (s.i & 1) != 0);
+    s.poll_mark = s.issued;
+    s.poll_tile = s.hcur >> 8;
     setf(s, F_GO_POLL, false);
 }
 
 // Every piece of the halo cursor's item at once (slow path and prologue).
 __device__ __forceinline__ void stage_h_block(const DCtx& c, DStream& s) {
     setf(s, F_GO_H, true);
-    s.hso = halo_src(c, s.hcur, __builtin_amdgcn_readfirstlane(tbl_hbase(cK(s.hcur))));
+    s.hso = halo_src(c, s.hcur, s.hinf, __builtin_amdgcn_readfirstlane(tbl_hbase(cK(s.hcur))));
     stage_h_piece<0>(c, s);
     stage_h_piece<1>(c, s);
     stage_h_piece<2>(c, s);
@@ -305,10 +341,12 @@ __device__ __forceinline__ void d_force_publish(const DCtx& c, DStream& s) {
 // own pending tile), then wait for this wave's pieces and make every wave's visible.
 __device__ __forceinline__ void d_slow_path(const DCtx& c, DStream& s) {
     const int i = s.i;
+    trunkd_count(0);
     if (s.wi <= i) stage_w_block(c, s);  // (weights never wait on anything: normally staged)
     if (s.hi <= i) {
         setf(s, F_POLL, false);  // an outstanding poll would be read for the cursor's tile after it moved
-        if (cur_needs_dep(c, s.hcur) && !has(s, F_HDEP)) {
+        if (cur_needs_dep(s.hcur, s.hinf) && !has(s, F_HDEP)) {
+            trunkd_count(1);
             d_force_publish(c, s);
             if (!(c.abl & 16)) {
                 const int nb = nb_of_pos(c, tbl_pos(cK(s.hcur)));
@@ -318,7 +356,7 @@ __device__ __forceinline__ void d_slow_path(const DCtx& c, DStream& s) {
         }
         stage_h_block(c, s);
         // refill the ring while the dependency is known to hold (same tile)
-        while (s.hi <= i + 2 && cL(s.hcur) < c.nl && (!cur_needs_dep(c, s.hcur) || has(s, F_HDEP)))
+        while (s.hi <= i + 2 && cL(s.hcur) < c.nl && (!cur_needs_dep(s.hcur, s.hinf) || has(s, F_HDEP)))
             stage_h_block(c, s);
     }
     if (s.wi <= i + 1 && cL(s.wcur) < c.nl) stage_w_block(c, s);
@@ -338,7 +376,7 @@ __device__ __forceinline__ void d_slow_path(const DCtx& c, DStream& s) {
 // (weights of i+2, halo of up to i+3).  Returns this lane's neighbour of the halo cursor's tile
 // (for a poll to issue).
 template <bool MORE>
-__device__ __forceinline__ int d_barrier(const DCtx& c, DStream& s) {
+__device__ __forceinline__ int d_barrier(const DCtx& c, DStream& s, int sL, int sk, int sch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int i = s.i;
     const bool next_staged = s.wi > i + 1 && s.hi > i + 1;  // (the cursors stop at the stream's end)
@@ -352,26 +390,33 @@ __device__ __forceinline__ int d_barrier(const DCtx& c, DStream& s) {
     if (s.pend >= 0) want(s.pend_mark);
     if (has(s, F_POLL)) want(s.poll_mark);
     if (any) wait_vm(s.issued - tgt);
+    trunkd_stamp(sL, sk, sch, 3);
     // the halo cursor's tile: read before the barrier (its lgkmcnt(0) covers the reads)
     int hk = cK(s.hcur);
     uint32_t hb = tbl_hbase(hk), hpos = tbl_pos(hk);
     raw_barrier();
+    trunkd_stamp(sL, sk, sch, 4);
     setf(s, F_READY, next_staged);
     if (s.pend >= 0) d_publish(c, s);
     int nb = nb_of_pos(c, hpos);
     // the poll issued at an earlier barrier has landed in its slot: the neighbourhood's verdict
-    if (has(s, F_POLL)) {
+    if (has(s, F_POLL) && s.poll_tile == (s.hcur >> 8)) {  // (a poll of a tile the cursor has left is void)
         const int lane = threadIdx.x & 63;
         const unsigned v = *reinterpret_cast<const volatile unsigned*>(smem + td::POLL_OFF +
                                                                        (has(s, F_POLLP) ? 256 : 0) + lane * 4);
         const unsigned need = c.gen * 1024u + (unsigned)cL(s.hcur);  // done with layer L - 1
-        if (__all(nb < 0 || (int)(v - need) >= 0)) setf(s, F_HDEP, true);
-        setf(s, F_POLL, false);
+        if (__all(nb < 0 || (int)(v - need) >= 0)) {
+            setf(s, F_HDEP, true);
+            trunkd_count(5);
+        }
     }
+    setf(s, F_POLL, false);
     if (MORE && !next_staged) {
+        trunkd_count(2);
         if (s.wi <= i + 1) stage_w_block(c, s);
         if (s.hi <= i + 1) {
-            if (cur_needs_dep(c, s.hcur) && !has(s, F_HDEP)) {
+            if (cur_needs_dep(s.hcur, s.hinf) && !has(s, F_HDEP)) {
+                trunkd_count(3);
                 if (!(c.abl & 16)) dep_wait(c.state, nb, c.gen * 1024u + (unsigned)cL(s.hcur), c.gen);
                 setf(s, F_HDEP, true);
             }
@@ -389,12 +434,17 @@ __device__ __forceinline__ int d_barrier(const DCtx& c, DStream& s) {
     // halo of the next unstaged item up to i+3 (its slot held item hi-3 <= i)
     setf(s, F_GO_H, false);
     if (s.hi <= i + 3 && cL(s.hcur) < c.nl) {
-        if (!cur_needs_dep(c, s.hcur) || has(s, F_HDEP) || (c.abl & 16)) {
+        if (!cur_needs_dep(s.hcur, s.hinf) || has(s, F_HDEP) || (c.abl & 16)) {
             setf(s, F_GO_H, true);
-            s.hso = halo_src(c, s.hcur, __builtin_amdgcn_readfirstlane(hb));
-        } else {
-            setf(s, F_GO_POLL, true);
+            s.hso = halo_src(c, s.hcur, s.hinf, __builtin_amdgcn_readfirstlane(hb));
         }
+    }
+    // poll the cursor tile's neighbourhood from the tile's first chunk on (not only once the
+    // cursor stands at a chunk that needs it): the verdict is one barrier old when it is read
+    if (cL(s.hcur) > 0 && cL(s.hcur) < c.nl && !has(s, F_HDEP) && !(c.abl & 16) &&
+        inf_fnew(s.hinf) != tk::NEED_NONE) {
+        setf(s, F_GO_POLL, true);
+        trunkd_count(4);
     }
     return nb;
 }
@@ -407,6 +457,7 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int R = td::R, CT = 32 * NF, TN = 3;
     const int wave = wave_id(), lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
+    const bool grp_b = wave >= 4;
     const int t = c.b + k * c.G, nch = rec_nch(rec);
     const uint32_t pos = __builtin_amdgcn_readfirstlane(tbl_pos(k));
     const int img = (int)(pos & 1023), by = (int)((pos >> 10) & 2047), bx = (int)(pos >> 21);
@@ -465,10 +516,12 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
         constexpr int FF = decltype(fold_tag)::value;            // fold target fragment (chunks 0..3), or -1
         constexpr bool FIRST = decltype(first_tag)::value != 0;  // the tile's chunk 0: nothing prefetched
         const int it = s.i;
+        trunkd_stamp(L, k, ch, 0);
         if constexpr (FIRST) {
             if (!has(s, F_READY)) d_slow_path(c, s);
             read_step0(it, P);
         }
+        trunkd_stamp(L, k, ch, 1);
         setf(s, F_READY, false);
         int pnb = -1;
         if (ch == 0) {
@@ -493,7 +546,9 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
             const int cur = (P + stp) & 1;
             if (stp == 2) {
                 __builtin_amdgcn_s_setprio(0);
-                pnb = d_barrier<MORE>(c, s);
+                trunkd_stamp(L, k, ch, 2);
+                pnb = d_barrier<MORE>(c, s, L, k, ch);
+                trunkd_stamp(L, k, ch, 5);
                 __builtin_amdgcn_s_setprio(1);
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -509,7 +564,9 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
                         else if (MORE) read_one(it + 1, 0, TN * NF + r + dyi, cur ^ 1);
                     }
                     // spread staging
-                    const int q = dyi * R + r;
+                    // waves 0-3 and their SIMD partners 4-7 issue at positions 6 rows apart, so
+                    // the two waves of a SIMD never stall on LDS-DMA issue at the same MFMA
+                    const int q = dyi * R + r - (grp_b ? 6 : 0);
                     if (stp == 0) {
                         if (q == 0) stage_h_piece<0>(c, s);
                         if (q == 1) stage_h_piece<1>(c, s);
@@ -552,6 +609,7 @@ __device__ __forceinline__ void d_run_tile(const DCtx& c, DStream& s, const_rec&
             }
         }
         __builtin_amdgcn_s_setprio(0);
+        trunkd_stamp(L, k, ch, 6);
         ++s.i;
     };
 
@@ -693,6 +751,7 @@ __global__ __launch_bounds__(td::NT, 2) void trunk_deep_kernel(unsigned* state, 
     c.b = blockIdx.x;
     const int ntiles = g.ntiles;
     c.my_tiles = c.b < ntiles ? (ntiles - 1 - c.b) / c.G + 1 : 0;
+    c.nbxy = (uint32_t)g.nbx | (uint32_t)g.nby << 16;
     c.pstride = (uint32_t)(g.hp * g.wp * 32);
     c.abytes = (uint32_t)((size_t)g.n * g.cs16 * c.pstride);  // < 2 GiB (prep err bit 64)
     c.abl = trunkd_abl();
@@ -721,9 +780,11 @@ __global__ __launch_bounds__(td::NT, 2) void trunk_deep_kernel(unsigned* state, 
     s.fl = 0;
     s.hso = 0;
     s.poll_mark = 0;
+    s.poll_tile = 0;
     s.pend = -1;
     s.pend_mark = 0;
     s.wcur = s.hcur = 0;
+    s.winf = s.hinf = lay_info(c, 0);
     s.wi = s.hi = 0;
     if (c.my_tiles > 0) {
         // prologue: weights of items 0, 1 and the halo of items 0..2 (layer 0 reads the trunk
@@ -731,7 +792,7 @@ __global__ __launch_bounds__(td::NT, 2) void trunk_deep_kernel(unsigned* state, 
         stage_w_block(c, s);
         stage_w_block(c, s);  // (every stream has >= 2 items: nch >= 2)
         stage_h_block(c, s);
-        while (s.hi < 3 && cL(s.hcur) < c.nl && !cur_needs_dep(c, s.hcur)) stage_h_block(c, s);
+        while (s.hi < 3 && cL(s.hcur) < c.nl && !cur_needs_dep(s.hcur, s.hinf)) stage_h_block(c, s);
         for (int L = 0; L < nl; ++L) {
             const_rec& rec = c.recs[L];
             const bool growth = rec_kind(rec) == 0;
@@ -779,8 +840,21 @@ int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s) {
 int trunk_deep_knobs_set(const int* k) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_trunkd_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
 }
+int trunk_deep_stamps_set(void* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trunkd_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+int trunk_deep_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trunkd_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_trunkd_stats), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
 #else
 int trunk_deep_knobs_set(const int*) { return -2; }
+int trunk_deep_stats(unsigned long long*, int) { return -2; }
+int trunk_deep_stamps_set(void*) { return -2; }
 #endif
 
 }  // namespace isr

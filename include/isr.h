@@ -398,6 +398,10 @@ int isr_tuning_trunk_stamps(void* buf);
  * waits;
  * per_cu > 0 caps the resident workgroups per CU (the grid). */
 int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k3);
+/* Tuning builds only: the deep-ring trunk's (variant 4) event counters since the last reset
+ * (uint64[8]: top slow paths, their blocking waits, mid-chunk slow paths, their blocking waits,
+ * neighbourhood polls issued, polls that found the neighbourhood done); reset != 0 zeroes them. */
+int isr_tuning_trunk_deep_stats(uint64_t* out, int32_t reset);
 /* Tuning builds only: per-item cycle stamps (s_memtime) of later production chain launches into
  * `buf` (uint64 [grid][2 layers: 77, 79][16 items][2 waves][8]: item top, own DMA landed, barrier
  * passed, refill issued, MFMAs issued) for each workgroup's first tile; NULL stops. */

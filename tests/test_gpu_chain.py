@@ -1,4 +1,4 @@
-"""The persistent RRDB-trunk kernel (isr_conv_chain, conv3x3.hip): the whole trunk of
+"""The persistent RRDB-trunk kernel (isr_conv_chain: trunk.hip, trunk_deep.hip, conv3x3.hip): the whole trunk of
 RDB convs in one launch with tile-level dependencies must reproduce the per-conv
 launches BIT FOR BIT (same tile arithmetic; only the hand-off differs: sc1 loads /
 write-through stores, progress words).  Repeated launches stress the hand-off for
@@ -63,8 +63,8 @@ def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks):
     gw = _gw(blocks)
     xs = _inputs(n, h, w, 3, seed=3)
     refs = _run(gw, xs, chain=False)
-    # variant 3 (32x32 tiles) needs the 16-row-rounded height to be a multiple of 32
-    for variant in (0, 2, 1) + ((3,) if -(-h // 16) % 2 == 0 else ()):
+    # variants 3 and 4 (32x32 tiles) need the 16-row-rounded height to be a multiple of 32
+    for variant in (0, 2, 1) + ((3, 4) if -(-h // 16) % 2 == 0 else ()):
         for acquire in (False, True):
             for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire, variant=variant), refs):
                 assert torch.equal(out, ref), \
