@@ -7,6 +7,9 @@ the repository snapshot to the GPU box.
 `python -m image_super_resolution_amd._build --tuning` builds lib/libisr_tuning.so
 with -DISR_TUNING (adds timing-only ablation variants whose outputs are wrong);
 tools load it with ISR_LIB=<path>.  The production libisr.so never contains them.
+`--interleave` builds lib/libisr_interleave.so: the production objects with trunk.hip rebuilt
+under -DISR_TRUNK_INTERLEAVE=1 (the trunk's refill pieces issued one per step-0 MFMA; kept for
+the parity run tests/test_gpu_chain.py gets with ISR_LIB pointing at it).
 """
 from __future__ import annotations
 
@@ -76,5 +79,29 @@ def build(force: bool = False, verbose: bool = False, tuning: bool = False) -> P
     return lib_path
 
 
+def build_interleave(verbose: bool = False) -> Path:
+    """libisr_interleave.so: production objects, trunk.hip with -DISR_TRUNK_INTERLEAVE=1."""
+    build(verbose=verbose)
+    objdir = PKG / "build_interleave"
+    objdir.mkdir(exist_ok=True)
+    trunk_obj = objdir / "trunk.o"
+    cmd = [HIPCC, *FLAGS, "-DISR_TRUNK_INTERLEAVE=1", "-c", str(CSRC / "trunk.hip"), "-o", str(trunk_obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed on trunk.hip (interleave):\n{r.stderr}")
+    objs = [trunk_obj if src.stem == "trunk" else PKG / "build" / (src.stem + ".o") for src in sources()]
+    lib_path = LIBDIR / "libisr_interleave.so"
+    tmp = lib_path.with_suffix(".so.tmp")
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    os.replace(tmp, lib_path)
+    return lib_path
+
+
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, tuning="--tuning" in sys.argv))
+    if "--interleave" in sys.argv:
+        print(build_interleave(verbose=True))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True, tuning="--tuning" in sys.argv))

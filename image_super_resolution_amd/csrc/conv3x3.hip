@@ -203,7 +203,7 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
                 }
                 if constexpr (MODE & 16) {  // LeakyReLU' of the (shuffled-grid) mask source, all channels
                     const bf16x8 mq =
-                        load16_hx<HX>(d.m, view_at(d.m, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8));
+                        load16_hx<HX>(d.m, d.n, view_at(d.m, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8));
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
                         if (!((float)mq[k] > 0.f)) v[k] *= d.mslope;
@@ -212,7 +212,7 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
 #pragma unroll
                     for (int k = 0; k < 8; ++k) v[k] = 0.f;
                 }
-                store8_bf16_hx<HX>(d.y, view_at(d.y, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8), v);
+                store8_bf16_hx<HX>(d.y, d.n, view_at(d.y, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8), v);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
@@ -240,11 +240,11 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
             for (int blk = 0; blk < 2; ++blk) {
                 const int co = cf + 16 * blk + 8 * hh;
                 if constexpr (MODE & 1) {
-                    if (use_r1) q1[buf][blk] = load16_hx<HX>(d.r1, view_at(d.r1, img, yy, xx, co));
+                    if (use_r1) q1[buf][blk] = load16_hx<HX>(d.r1, d.n, view_at(d.r1, img, yy, xx, co));
                 }
-                if constexpr (MODE & 2) q2[buf][blk] = load16_hx<HX>(d.r2, view_at(d.r2, img, yy, xx, co));
+                if constexpr (MODE & 2) q2[buf][blk] = load16_hx<HX>(d.r2, d.n, view_at(d.r2, img, yy, xx, co));
                 if constexpr (MODE & 16) {
-                    if (use_m) qm[buf][blk] = load16_hx<HX>(d.m, view_at(d.m, img, yy, xx, co));
+                    if (use_m) qm[buf][blk] = load16_hx<HX>(d.m, d.n, view_at(d.m, img, yy, xx, co));
                 }
             }
         };
@@ -291,8 +291,8 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
                     if (!valid) u[e] = 0.f;
                 }
                 const int co = cf + 16 * blk + 8 * hh;
-                store8_bf16_hx<HX>(d.y, view_at(d.y, img, yy, xx, co), u);
-                if constexpr (MODE & 4) store8_bf16_hx<HX>(d.y2, view_at(d.y2, img, yy, xx, co), u);
+                store8_bf16_hx<HX>(d.y, d.n, view_at(d.y, img, yy, xx, co), u);
+                if constexpr (MODE & 4) store8_bf16_hx<HX>(d.y2, d.n, view_at(d.y2, img, yy, xx, co), u);
             }
         }
     }
@@ -532,7 +532,11 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
                     fb[set][dyi][f] = lds_read16(ws + u * 16);
                 } else {
                     const int ia = idx - TN * NF;
-                    const int q = qw + (TLO + ia) * C::HC + dx;
+                    int qb = qw;
+                    // fold kernels: the row's swizzled address is recomputed at each read (an opaque
+                    // copy of qw) — hoisted, the peeled fold chunks kept ~18 of them live and spilled
+                    if constexpr (C::FOLD) asm volatile("" : "+v"(qb));
+                    const int q = qb + (TLO + ia) * C::HC + dx;
                     fa[set][ia] = lds_read16(hs + ks * C::HIPL * 1024 + halo_unit2(q, hh) * 16);
                 }
             };

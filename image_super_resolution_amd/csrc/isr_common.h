@@ -115,18 +115,22 @@ __device__ __forceinline__ void store8_bf16(char* p, const float* v) {
 // 16-byte load / 8-channel bf16 store at `p` inside view `v`: plain (HX = 0), or the hand-off
 // form (HX = 1: sc1 load that bypasses L1; write-through sc1 store, Guideline 16 R1) through a
 // buffer descriptor built from the view's base (wave-uniform: no waterfall) with the byte
-// offset as the per-lane voffset — hand-off buffers are far below the 2 GiB window.
+// offset as the per-lane voffset — hand-off buffers are far below the 2 GiB window.  num_records
+// is the view's real extent (n images of cs/16 planes), so a stray offset reads zeros or drops
+// the store instead of reaching past the allocation.
 template <class V>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const V& v) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(v.data), (short)0, 0x7fffffff, 0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const V& v, int n) {
+    const size_t bytes = (size_t)n * (v.cs >> 4) * v.hp * v.wp * 32;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(v.data), (short)0,
+                                             (int)(bytes < 0x7fffffffull ? bytes : 0x7fffffffull), 0x00020000);
 }
 
 template <int HX, class V>
-__device__ __forceinline__ bf16x8 load16_hx(const V& v, const char* p) {
+__device__ __forceinline__ bf16x8 load16_hx(const V& v, int n, const char* p) {
     if constexpr (HX) {
         typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
         const int off = (int)(p - (const char*)v.data);
-        u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(v), off, 0, 16);
+        u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(v, n), off, 0, 16);
         return __builtin_bit_cast(bf16x8, r);
     } else {
         return *reinterpret_cast<const bf16x8*>(p);
@@ -134,14 +138,14 @@ __device__ __forceinline__ bf16x8 load16_hx(const V& v, const char* p) {
 }
 
 template <int HX, class V>
-__device__ __forceinline__ void store8_bf16_hx(const V& v, char* p, const float* x) {
+__device__ __forceinline__ void store8_bf16_hx(const V& v, int n, char* p, const float* x) {
     bf16x8 t;
 #pragma unroll
     for (int e = 0; e < 8; ++e) t[e] = (__bf16)x[e];
     if constexpr (HX) {
         typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
         const int off = (int)(p - (const char*)v.data);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), rsrc_of(v), off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), rsrc_of(v, n), off, 0, 16);
     } else {
         *reinterpret_cast<bf16x8*>(p) = t;
     }

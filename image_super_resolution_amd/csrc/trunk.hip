@@ -218,6 +218,7 @@ struct Src {
     const char* w;   // packed weights of chunk 0
     const float* b;  // bias
     int wpc;         // weight pieces per chunk (9 / 18)
+    uint32_t xbytes, wbytes;  // extents of the activation buffer and of the packed weights
 };
 
 template <class K>
@@ -228,6 +229,7 @@ struct TrunkCtx {
     int acquire;
     int hp, wp, cs16, pad, h, w, nbx, nby, ntiles;
     uint32_t pstride;            // bytes per 16-channel plane
+    uint32_t abytes;             // bytes of one activation buffer (< 2 GiB: prep err bit 64)
     uint32_t hoff[K::HPW];       // per-lane halo piece offsets (chunk-invariant)
     int abl;                     // tuning ablation bits (0 in production builds)
 };
@@ -242,6 +244,8 @@ __device__ __forceinline__ Src src_of(const C& c, const_rec& rec, int t) {
     s.w = (const char*)(uintptr_t)rec.w;
     s.b = (const float*)(uintptr_t)rec.b;
     s.wpc = rec_kind(rec) == 0 ? tk::WPG : tk::WPF;
+    s.xbytes = c.abytes;
+    s.wbytes = (uint32_t)(rec_nch(rec) * s.wpc * 1024);
     return s;
 }
 
@@ -256,7 +260,7 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
     const int wave = wave_id(), lane = threadIdx.x & 63;
     char* dst = smem + slot * SLOTB;
     uint32_t n = 0;
-    const auto rx = rsrc(s.x);
+    const auto rx = rsrc_n(s.x, s.xbytes);
     const uint32_t so = s.h0 + (uint32_t)chunk * pstride;
     if (!(abl & 1)) {
 #pragma unroll
@@ -268,7 +272,7 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
             }
         }
     }
-    const auto rw = rsrc(s.w);
+    const auto rw = rsrc_n(s.w, s.wbytes);
     const uint32_t wo = (uint32_t)(chunk * s.wpc * 1024);
     char* wd = dst + HP * 1024;
 #pragma unroll
@@ -281,7 +285,7 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
     }
     if (with_bias && wave == 0) {
         if (lane < (s.wpc == tk::WPG ? 32 : 64))  // cout floats only
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(s.b), ISR_LDS_PTR(smem + BIASB + bslot * 256), 4,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(s.b, s.wpc == tk::WPG ? 128u : 256u), ISR_LDS_PTR(smem + BIASB + bslot * 256), 4,
                                                      lane * 4, 0, 0, 0);
         ++n;
     }
@@ -291,6 +295,19 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
 template <class K>
 __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src& s, int chunk, int slot, bool with_bias,
                                                 int bslot) {
+#ifdef ISR_TUNING
+    // tuning-build check of the ring protocol: the chunk lies inside the layer (chunk < nch: its
+    // weights inside the packed table) and the slot inside the ring.  A violation gives the launch
+    // up (the host raises) and issues nothing, instead of a DMA to a wrong place.
+    if (chunk < 0 || (uint32_t)(chunk * s.wpc * 1024) >= s.wbytes || slot < 0 || slot >= K::NST ||
+        bslot < 0 || bslot > 3) {
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(c.state + 1, c.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(c.state + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return 0;
+    }
+#endif
     return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF, K::HP>(c.hoff, c.pstride, c.abl, s, chunk, slot,
                                                                       with_bias, bslot);
 }
@@ -346,7 +363,7 @@ __device__ __forceinline__ uint32_t refill_piece_k(const uint32_t* hoff, int abl
     if (p < HPW) {
         const int j = wave + WM * p;
         if (!(abl & 1) && j < HP) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.x), ISR_LDS_PTR(rf.dst + j * 1024), 16, hoff[p],
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(rf.src.x, rf.src.xbytes), ISR_LDS_PTR(rf.dst + j * 1024), 16, hoff[p],
                                                      rf.so, 0, 16);
             return 1;
         }
@@ -355,7 +372,7 @@ __device__ __forceinline__ uint32_t refill_piece_k(const uint32_t* hoff, int abl
     if (p < HPW + WPW) {
         const int j = wave + WM * (p - HPW);
         if (j < rf.src.wpc) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.w), ISR_LDS_PTR(rf.dst + (HP + j) * 1024), 16,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(rf.src.w, rf.src.wbytes), ISR_LDS_PTR(rf.dst + (HP + j) * 1024), 16,
                                                      lane * 16, rf.wo + j * 1024, 0, 0);
             return 1;
         }
@@ -363,7 +380,7 @@ __device__ __forceinline__ uint32_t refill_piece_k(const uint32_t* hoff, int abl
     }
     if (p == HPW + WPW && rf.bias && wave == 0) {
         if (lane < (rf.src.wpc == tk::WPG ? 32 : 64))  // cout floats only
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(rf.src.b), ISR_LDS_PTR(smem + BIASB + rf.bslot * 256), 4,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(rf.src.b, rf.src.wpc == tk::WPG ? 128u : 256u), ISR_LDS_PTR(smem + BIASB + rf.bslot * 256), 4,
                                                      lane * 4, 0, 0, 0);
         return 1;
     }
@@ -387,6 +404,15 @@ __device__ __forceinline__ Refill make_refill(const TrunkCtx<K>& c, const Src& s
     rf.dst = smem + slot * K::SLOT;
     rf.bias = with_bias;
     rf.bslot = bslot;
+#ifdef ISR_TUNING
+    if (chunk < 0 || rf.wo >= s.wbytes || slot < 0 || slot >= K::NST || bslot < 0 || bslot > 3) {
+        if (threadIdx.x == 0) {  // as in stage_chunk: give the launch up, issue nothing
+            __hip_atomic_store(c.state + 1, c.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(c.state + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        rf.on = false;
+    }
+#endif
     return rf;
 }
 
@@ -684,7 +710,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     {
         typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
         const int xx = x0 + l31;
-        const auto yr = __builtin_amdgcn_make_buffer_rsrc((char*)(uintptr_t)rec.y, (short)0, 0x7fffffff, 0x00020000);
+        const auto yr = rsrc_n((const void*)(uintptr_t)rec.y, c.abytes);
         const float slope = rec.slope, s1 = rec.s1, s2 = rec.s2;
         const bool scale2 = s2 != 1.f;
         const uint32_t plane_px = (uint32_t)(c.hp * c.wp);
@@ -695,7 +721,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
         // Compiler-visible loads: hipcc places the wait before their first use itself.
         bf16x8 q2[R][NF][2];
         const uint32_t r2pl = (uint32_t)(img * c.cs16 + rec_r2p(rec)) * plane_px;
-        const auto rr = rsrc((const char*)(uintptr_t)rec.r2);
+        const auto rr = rsrc_n((const void*)(uintptr_t)rec.r2, c.abytes);
         auto load_r2 = [&](int r) {
             const uint32_t pix = (uint32_t)((y0 + wave * R + r + c.pad) * c.wp + xx + c.pad);
 #pragma unroll
@@ -785,6 +811,7 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
     c.nby = g.nby;
     c.ntiles = g.ntiles;
     c.pstride = (uint32_t)(c.hp * c.wp * 32);
+    c.abytes = (uint32_t)((size_t)g.n * g.cs16 * c.pstride);
     c.abl = trunk_abl_load();
     {
         const int wave = wave_id(), lane = threadIdx.x & 63;

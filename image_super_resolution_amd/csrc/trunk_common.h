@@ -95,8 +95,10 @@ __device__ __forceinline__ void acquire_fence() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+// Buffer resource over [p, p + bytes): num_records is the tensor's real extent, so an offset past
+// it reads zeros / drops the store instead of touching whatever lies beyond the allocation.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_n(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
 // LDS halo image of one chunk: pixel q = row * 34 + col holds 2 units of 16 B (8 channels);

@@ -83,10 +83,6 @@ __device__ __forceinline__ void trunkd_count(int) {}
 __device__ __forceinline__ void trunkd_stamp(int, int, int, int) {}
 #endif
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_n(const void* p, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-
 // Per-workgroup tile table in LDS (written once at kernel start; the workgroup's tiles are
 // t = b + k G for k < my_tiles, the same list on every layer): [k] = {halo origin byte offset of
 // the tile at plane 0 of its image: pixel (y0 - 1, x0 - 1); img | by << 10 | bx << 21}.  Keeps the

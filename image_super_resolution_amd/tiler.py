@@ -23,6 +23,7 @@ halo=0 mode:
 from __future__ import annotations
 
 import heapq
+import os
 import warnings
 from collections import defaultdict
 from dataclasses import dataclass
@@ -122,6 +123,61 @@ def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | N
     return out
 
 
+def plan_blocks(height: int, width: int, world: int, halo: int, limit: int = 2 ** 31) -> list[list[Tile]]:
+    """Multi-GPU deal of a still as a 2-D grid of blocks: gr x gc = world x k
+    blocks of equal core (split evenly: cores differ by at most one pixel), each extended by `halo` LR pixels on every
+    side and clipped at the image edge (a true image edge is the network's own zero padding, so
+    clipping loses no context the whole-image forward has); rank r takes blocks [r k, (r + 1) k)
+    in raster order.  k is the smallest count whose blocks fit the trunk kernel's 2 GiB buffer
+    window; among the grids of that count the one with the least work on the busiest rank wins
+    (work = the blocks' tile-aligned LR area, what the trunk kernel computes).  Full-width bands
+    are the gc = 1 member of this family; at cfg4 over 8 ranks the 2 x 4 grid puts 1.14 M LR px
+    on the busiest rank against 1.29 M for the 334-row bands (halo 32: 8 % vs 24 % overhead).
+    Returns per-rank Tile lists (raster order inside a rank)."""
+    from .ops import TILE_H, TILE_W, round_up
+    if world < 1 or halo < 0 or height < 1 or width < 1:
+        raise ValueError("plan_blocks: world >= 1, halo >= 0 and a non-empty image required")
+
+    def grid(gr: int, gc: int) -> list[Tile]:
+        ys = [i * height // gr for i in range(gr + 1)]  # even split: cores differ by <= 1 pixel
+        xs = [j * width // gc for j in range(gc + 1)]
+        out = []
+        for i in range(gr):
+            for j in range(gc):
+                y, x, h, w = ys[i], xs[j], ys[i + 1] - ys[i], xs[j + 1] - xs[j]
+                out.append(Tile(len(out), y, x, h, w, max(0, y - halo), max(0, x - halo),
+                                min(height, y + h + halo), min(width, x + w + halo)))
+        return out
+
+    def fits(t: Tile) -> bool:
+        h, w = t.in_shape
+        return 192 * 2 * (round_up(h, TILE_H) + 2) * (round_up(w, TILE_W) + 2) < limit
+
+    k = 1
+    while True:
+        n = world * k
+        best = None
+        for gr in range(1, n + 1):
+            if n % gr:
+                continue
+            gc = n // gr
+            if gr > height or gc > width:
+                continue
+            blocks = grid(gr, gc)
+            if not all(fits(t) for t in blocks):
+                continue  # too big for the window
+            work = max(sum(round_up(t.in_shape[0], TILE_H) * round_up(t.in_shape[1], TILE_W)
+                           for t in blocks[r * k:(r + 1) * k]) for r in range(world))
+            if best is None or work < best[0]:
+                best = (work, blocks)
+        if best is not None:
+            blocks = best[1]
+            return [blocks[r * k:(r + 1) * k] for r in range(world)]
+        if n > height * width:
+            raise ValueError("plan_blocks: no grid fits the buffer window")
+        k += 1
+
+
 def band_max_rows(width: int, limit: int = 2 ** 31) -> int:
     """Largest band input height whose 192-channel dense buffer (engine.GeneratorBuffers:
     bf16, 16x32-rounded, 1-px border) stays below the trunk kernel's 2 GiB buffer window."""
@@ -218,32 +274,42 @@ class TileUpscaler:
     """
 
     def __init__(self, runner: BatchRunner, scale: int, window: int = 96, halo: int = 0, batch: int = 8,
-                 device="cuda", shard: str = "windows"):
+                 device="cuda", shard: str = "windows", gather: str = "device"):
         """`shard`: "windows" runs rs.py's windows (dealt longest-processing-time-first over
         ranks, shard_tiles; the canvas equals the single-rank one bit for bit); "bands" runs
         full-width horizontal bands with the same halo (plan_bands: one rank's share is one or a
         few bands of one input shape, one batch-1 forward each — `batch` applies to windows only;
         on one GPU the image splits into as few bands as the trunk kernel's 2 GiB buffer window
         allows; needs halo > 0 to hide its seams, and differs from the windowed canvas by the
-        seams each form leaves)."""
+        seams each form leaves); "blocks" runs a 2-D grid of blocks with the same halo (plan_blocks:
+        at cfg4 over 8 ranks 2 x 4 blocks, 8 % halo work instead of the bands' 24 %).
+        `gather` (world > 1): "device" sends every finished tile to rank 0's device canvas point to
+        point; "host" has every rank copy its tiles (device → pinned host) into one shared host canvas
+        (a file in /dev/shm, all ranks on one node) that rank 0 returns as a CPU tensor — the
+        still's output is written from host memory anyway (rs.py: cv2.imwrite), and the ranks' D2H
+        copies run in parallel over their own links instead of one after another into rank 0."""
         if batch < 1:
             raise ValueError("batch must be >= 1")
-        if shard not in ("windows", "bands"):
-            raise ValueError(f"shard must be 'windows' or 'bands', got {shard!r}")
-        if shard == "bands" and halo == 0:
-            warnings.warn("shard='bands' with halo=0: the bands' seams are not hidden (pass halo > 0)",
-                          stacklevel=2)
-        if shard == "bands" and batch != 1:
-            warnings.warn(f"shard='bands' runs every band as one batch-1 forward; batch={batch} is ignored",
-                          stacklevel=2)
+        if shard not in ("windows", "bands", "blocks"):
+            raise ValueError(f"shard must be 'windows', 'bands' or 'blocks', got {shard!r}")
+        if gather not in ("device", "host"):
+            raise ValueError(f"gather must be 'device' or 'host', got {gather!r}")
+        if shard != "windows" and halo == 0:
+            warnings.warn(f"shard={shard!r} with halo=0: the seams are not hidden (pass halo > 0)", stacklevel=2)
+        if shard != "windows" and batch != 1:
+            warnings.warn(f"shard={shard!r} runs every band / block as one batch-1 forward; batch={batch} is "
+                          "ignored", stacklevel=2)
         self.runner, self.scale, self.window, self.halo, self.batch = runner, scale, window, halo, batch
         self.device = torch.device(device)
         self.shard = shard
+        self.gather = gather
 
     def shards(self, height: int, width: int, world: int) -> list[list[Tile]]:
         """The per-rank tile lists of an image (deterministic: every rank computes the same)."""
         if self.shard == "bands":
             return plan_bands(height, width, world, self.halo)
+        if self.shard == "blocks":
+            return plan_blocks(height, width, world, self.halo)
         tiles = plan_tiles(height, width, self.window, self.halo)
         return shard_tiles(tiles, world) if world > 1 else [tiles]
 
@@ -256,7 +322,7 @@ class TileUpscaler:
             groups[t.in_shape].append(t)
         out: dict[int, torch.Tensor] = {}
         # bands are sized to the trunk kernel's 2 GiB buffer window one at a time: batch 1
-        step = 1 if self.shard == "bands" else self.batch
+        step = 1 if self.shard != "windows" else self.batch
         for (h, w), lst in groups.items():
             for i in range(0, len(lst), step):
                 chunk = lst[i:i + step]
@@ -287,12 +353,59 @@ class TileUpscaler:
         verify = getattr(self.runner, "verify", None)
         if verify is not None:
             verify()  # every forward of this image, the last included, before anything is stitched
+        if self.gather == "host":
+            return _gather_host(mine, done, s, (c, H * s, W * s), rank, world, group)
         if world == 1:
             canvas = torch.zeros((c, H * s, W * s), dtype=torch.uint8, device=self.device)
             for t in tiles:
                 canvas[:, t.y * s:(t.y + t.h) * s, t.x * s:(t.x + t.w) * s] = done[t.index]
             return canvas
         return _gather_to_rank0(tiles, shards, done, s, (c, H * s, W * s), rank, group, self.device)
+
+
+def copy_tiles_to_host(mine, done, s, canvas: torch.Tensor) -> None:
+    """Device → host copy of a rank's finished tiles into the CPU `canvas` (through one pinned
+    staging buffer per tile when the tiles live on a GPU; one synchronisation at the end)."""
+    staged = []
+    for t in mine:
+        part = done[t.index]
+        if part.is_cuda:
+            pin = torch.empty(part.shape, dtype=part.dtype, pin_memory=True)
+            pin.copy_(part, non_blocking=True)
+            staged.append((t, pin))
+        else:
+            canvas[:, t.y * s:(t.y + t.h) * s, t.x * s:(t.x + t.w) * s] = part
+    if staged:
+        torch.cuda.synchronize(done[mine[0].index].device)
+    for t, pin in staged:
+        canvas[:, t.y * s:(t.y + t.h) * s, t.x * s:(t.x + t.w) * s] = pin
+
+
+def _gather_host(mine, done, s, canvas_shape, rank, world, group):
+    """gather="host": every rank writes its tiles into one shared host canvas (module doc of
+    TileUpscaler.__init__); rank 0 returns it, the others None."""
+    import numpy as np
+    if world == 1:
+        canvas = torch.zeros(canvas_shape, dtype=torch.uint8)
+        copy_tiles_to_host(mine, done, s, canvas)
+        return canvas
+    import tempfile
+    import torch.distributed as dist
+    name = [None]
+    if rank == 0:
+        fd, name[0] = tempfile.mkstemp(prefix="isr_canvas_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        os.close(fd)
+        np.memmap(name[0], dtype=np.uint8, mode="w+", shape=canvas_shape).flush()  # sized, zero-filled
+    dist.broadcast_object_list(name, src=0, group=group)
+    try:
+        mm = np.memmap(name[0], dtype=np.uint8, mode="r+", shape=canvas_shape)
+        copy_tiles_to_host(mine, done, s, torch.from_numpy(mm))
+        dist.barrier(group=group)  # every rank's tiles are in the canvas
+        out = torch.from_numpy(mm) if rank == 0 else None  # rank 0 keeps the mapping (no copy)
+    finally:
+        if rank == 0:
+            os.unlink(name[0])  # the name only: the mapping lives as long as the returned tensor
+    return out
 
 
 def _gather_to_rank0(tiles, shards, done, s, canvas_shape, rank, group, device):

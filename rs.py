@@ -104,7 +104,8 @@ def runer(**kw):
     model = build_model(kw["model"], kw["add_rate"], mean, std)
     runner = tiler.runner_for(model, device)
     up = tiler.TileUpscaler(runner, runner.scale, window=kw["window_size"], halo=kw["halo"],
-                            batch=kw["batch_size"], device=device, shard=kw.get("shard", "windows"))
+                            batch=kw["batch_size"], device=device, shard=kw.get("shard", "windows"),
+                            gather=kw.get("gather", "device"))
     image = read_image(src)
     if rank == 0:
         print("input shape", tuple(image.shape))
@@ -131,9 +132,11 @@ if __name__ == "__main__":
     p.add_argument("--batch_size", type=int, default=1)
     p.add_argument("--worker", type=int, default=4, help="accepted for CLI compatibility (decode is in-process)")
     p.add_argument("--halo", type=int, default=0, help="LR pixels of context around each window (0 = reference)")
-    p.add_argument("--shard", choices=("windows", "bands"), default="windows",
-                   help="windows (the reference's, default) or full-width bands with the same halo: fewer, "
-                        "larger forwards (cfg4 on one MI355X: 576 vs 460 MPix/s with --halo 32)")
+    p.add_argument("--shard", choices=("windows", "bands", "blocks"), default="windows",
+                   help="windows (the reference's, default), full-width bands or a 2-D grid of blocks with the "
+                        "same halo: fewer, larger forwards (cfg4 on one MI355X: 576 vs 460 MPix/s with --halo 32)")
+    p.add_argument("--gather", choices=("device", "host"), default="device",
+                   help="multi-GPU: finished tiles to rank 0's device (p2p) or into one shared host canvas")
     p.add_argument("--add_rate", type=float, default=0.2)
     p.add_argument("--mean", type=float, nargs=3, default=(0.485, 0.456, 0.406))
     p.add_argument("--std", type=float, nargs=3, default=(0.229, 0.224, 0.225))

@@ -149,12 +149,14 @@ def _stitch(shards, done, shape):
     return canvas
 
 
+@pytest.mark.parametrize("shard", ["bands", "blocks"])
 @torch.no_grad()
-def test_cfg4_bands_vs_whole_image(setup):
-    """Each of 8 ranks' bands (one 334- or 302-row full-width band per rank) run on this GPU,
-    stitched: the canvas rank 0 would assemble, against one whole-image forward."""
+def test_cfg4_bands_vs_whole_image(setup, shard):
+    """Each of 8 ranks' share (bands: one 334-row full-width band per rank; blocks: one block of
+    the 2 x 4 grid, 1112 x 992 / 1024) run on this GPU, stitched: the canvas rank 0 would
+    assemble, against one whole-image forward."""
     r = setup["runner"]
-    up = tiler.TileUpscaler(r, S, window=WINDOW, halo=HALO, batch=1, device=DEV, shard="bands")
+    up = tiler.TileUpscaler(r, S, window=WINDOW, halo=HALO, batch=1, device=DEV, shard=shard)
     img = setup["img"].to(DEV)
     shards = up.shards(H, W, 8)
     assert all(len({t.in_shape for t in lst}) == 1 for lst in shards)
@@ -165,12 +167,13 @@ def test_cfg4_bands_vs_whole_image(setup):
     canvas = _stitch(shards, done, setup["canvas"].shape)
     whole = setup["model"](img[None])[0]
     err = (canvas.float() - whole.float()).abs().mean().item()
-    print(f"mean |bands - whole| (LSB): {err:.4f}")
+    print(f"mean |{shard} - whole| (LSB): {err:.4f}")
     assert err <= 0.5, err
 
 
+@pytest.mark.parametrize("shard", ["bands", "blocks"])
 @torch.no_grad()
-def test_bands_with_full_receptive_halo_equal_whole_image_bitwise():
+def test_bands_with_full_receptive_halo_equal_whole_image_bitwise(shard):
     """With a halo at least the network's receptive radius (ResNet(1) x4: 9x9 head 4 + 15 RDB
     convs + conv1 + the Scaler and 9x9 tail convs < 24 LR px) every band output pixel sees the
     same inputs and the same arithmetic as in one whole-image forward: bit-identical canvas."""
@@ -183,8 +186,8 @@ def test_bands_with_full_receptive_halo_equal_whole_image_bitwise():
     img = torch.randint(0, 256, (3, 150, 230), generator=g, dtype=torch.uint8).to(DEV)
     runner = tiler.runner_for(m, DEV)
     whole = m(img[None])[0]
-    up = tiler.TileUpscaler(runner, S, window=64, halo=24, batch=1, device=DEV, shard="bands")
-    for world in (2, 3):
+    up = tiler.TileUpscaler(runner, S, window=64, halo=24, batch=1, device=DEV, shard=shard)
+    for world in (2, 3, 4):
         shards = up.shards(150, 230, world)
         done = {}
         for lst in shards:

@@ -1,0 +1,122 @@
+"""Training at cfg3's per-GPU shape (train.py:70-129 `train_srgan`):
+SRGAN(16, 0.2, enchant=True, 4) — the 16-RRDB EResNet x4 generator — on a batch of 16 crops of
+512² HR / 128² LR, VGG19 conv5_4 L1 + adversarial loss, one step through trainer.train_srgan.
+
+* The same step with the training forward's trunk on the persistent trunk kernel and on 240
+  per-conv launches (ISR_TRAIN_CHAIN=0): the kernel is bit-identical to the per-conv launches
+  (tests/test_gpu_chain.py), so every generator gradient must agree bit for bit (asserted after
+  the test_gpu_train.py bar, rel L2 <= 5e-2 and cos >= 0.998, so a failure shows how far off).  Learning rates are 0, so the step leaves G and D unchanged and both runs see
+  the same discriminator and VGG.
+* A 2-sample slice of the batch (full 128² LR crops, the same 16 RRDBs) through a pixel-loss
+  step vs autograd of the fp32 oracle (oracle/ref_cpu.generator) at the test_gpu_train.py bars.
+"""
+import os
+import warnings
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from image_super_resolution_amd import data, loss as L, models, optim, trainer
+from image_super_resolution_amd.weights import synth_state_dict
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BLOCKS, SCALE, BATCH, HR = 16, 4, 16, 512
+
+
+@pytest.fixture(scope="module", autouse=True)
+def lib(built_lib):
+    return built_lib
+
+
+def _gen(seed):
+    g = models.SRGAN(BLOCKS, 0.2, True, SCALE)
+    g.load_state_dict(synth_state_dict(g.state_dict(), seed))
+    return g.to(DEV)
+
+
+def _srgan_step_grads(chain: bool, dis, gl):
+    """One train_srgan step (lr 0) with the trunk kernel on or off; the generator's gradients."""
+    old = os.environ.get("ISR_TRAIN_CHAIN")
+    os.environ["ISR_TRAIN_CHAIN"] = "1" if chain else "0"
+    try:
+        gen = _gen(5)
+        mean, std = list(data.IMAGENET_MEAN), list(data.IMAGENET_STD)
+        og = optim.FusedAdam(gen.parameters(), lr=0.0)
+        od = optim.FusedAdam(dis.parameters(), lr=0.0)
+        sg = torch.optim.lr_scheduler.LinearLR(og, 1, 0.01, total_iters=1)
+        sd = torch.optim.lr_scheduler.LinearLR(od, 1, 0.01, total_iters=1)
+        ema = models.ModelEMA(gen, tau=1)
+        ema.ema.to(DEV)
+        sc = (torch.amp.GradScaler("cuda", enabled=False), torch.amp.GradScaler("cuda", enabled=False))
+        tf = data.GPUTransform(SCALE, hr_norm=True, mean=mean, std=std, device=DEV)
+        batches = data.SyntheticSR(BATCH, HR, seed=3, device=DEV)
+        losses = trainer.train_srgan(gen, ema, dis, batches, tf, gl, og, od, sc, (sg, sd), 0, None, mean=mean,
+                                     std=std, steps=1, log_every=1)
+        torch.cuda.synchronize()
+        plan = gen.res_net.__dict__["_isr_train_plan"]
+        assert (plan.chain is not None) == chain, "trunk kernel on/off as requested"
+        return losses[0], {n: p.grad.detach().clone() for n, p in gen.named_parameters()}
+    finally:
+        if old is None:
+            os.environ.pop("ISR_TRAIN_CHAIN", None)
+        else:
+            os.environ["ISR_TRAIN_CHAIN"] = old
+
+
+def test_cfg3_srgan_step_chain_vs_per_conv():
+    torch.manual_seed(0)
+    dis = models.Discriminator(3, 64, 8, 1024).to(DEV)
+    dis.use_libisr(True)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        gl = L.gen_loss(device=DEV, beforeAct=True)
+    l_chain, g_chain = _srgan_step_grads(True, dis, gl)
+    l_conv, g_conv = _srgan_step_grads(False, dis, gl)
+    assert abs(l_chain - l_conv) <= 1e-4 * abs(l_conv) + 1e-6, (l_chain, l_conv)
+    bitwise = 0
+    worst = []
+    for name, gc in g_conv.items():
+        gk = g_chain[name]
+        bitwise += int(torch.equal(gk, gc))
+        rel = ((gk - gc).norm() / gc.norm().clamp_min(1e-12)).item()
+        cos = F.cosine_similarity(gk.flatten().double(), gc.flatten().double(), dim=0).item()
+        worst.append((rel, cos, name))
+        assert rel <= 5e-2 and cos >= 0.998, f"{name}: rel {rel:.3e} cos {cos:.5f}"
+    worst.sort(reverse=True)
+    print(f"cfg3 SRGAN step: content loss {l_chain:.6f} vs {l_conv:.6f}; {bitwise}/{len(g_conv)} generator "
+          f"gradients bitwise equal; worst {worst[:2]}")
+    # measured on MI355X: 490 / 490 bitwise (the trunk kernel and the per-conv launches compute
+    # every activation bit for bit alike, and the backward is the same code on both)
+    assert bitwise == len(g_conv), f"{len(g_conv) - bitwise} gradients differ (within the bars above)"
+
+
+def test_cfg3_two_sample_slice_vs_oracle():
+    gen = _gen(5)
+    batches = data.SyntheticSR(BATCH, HR, seed=3, device=DEV)
+    tf = data.GPUTransform(SCALE, hr_norm=True, device=DEV)
+    hr, lr = tf(next(batches))
+    hr, lr = hr[:2].float(), lr[:2].float()
+    sd = {k: v.detach().cpu().clone().float() for k, v in gen.res_net.state_dict().items()}
+    params = {k: v.requires_grad_(True) for k, v in sd.items() if v.is_floating_point()}
+    y_ref = R.generator(sd, lr.cpu(), num_blocks=BLOCKS, scale=SCALE, enchant=True)
+    ref_loss = F.mse_loss(y_ref, hr.cpu())
+    ref_loss.backward()
+
+    gen.train()
+    loss = F.mse_loss(gen(lr), hr)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert gen.res_net.__dict__["_isr_train_plan"].chain is not None
+    assert abs(loss.item() - ref_loss.item()) <= 1e-3 * abs(ref_loss.item()) + 1e-5, (loss.item(), ref_loss.item())
+    worst = []
+    for name, p in gen.res_net.named_parameters():
+        r = params[name].grad.to(DEV)
+        rel = ((p.grad - r).norm() / r.norm().clamp_min(1e-12)).item()
+        cos = F.cosine_similarity(p.grad.flatten(), r.flatten(), dim=0).item()
+        worst.append((rel, cos, name))
+        assert rel <= 5e-2 and cos >= 0.998, f"{name}: rel {rel:.3e} cos {cos:.5f}"
+    worst.sort(reverse=True)
+    print("cfg3 2-sample slice, worst grads vs oracle:", worst[:3])

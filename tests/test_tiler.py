@@ -115,6 +115,41 @@ def test_bands_single_rank_equals_whole_image():
     assert torch.equal(up(img), full)
 
 
+@pytest.mark.parametrize("h,w,world,halo", [(2160, 3840, 8, 32), (2160, 3840, 1, 32), (45, 61, 2, 2),
+                                             (45, 61, 3, 1), (5, 9, 8, 1), (100, 7, 4, 0)])
+def test_plan_blocks_cover_and_halo(h, w, world, halo):
+    """Blocks cover every LR pixel exactly once; each block's input is its core plus the halo on
+    every side, clipped to the image; every block fits the trunk kernel's buffer window."""
+    shards = tiler.plan_blocks(h, w, world, halo)
+    assert len(shards) == world and all(len(s) == len(shards[0]) for s in shards)
+    cover = torch.zeros(h, w, dtype=torch.int32)
+    for b in (b for s in shards for b in s):
+        cover[b.y:b.y + b.h, b.x:b.x + b.w] += 1
+        assert (b.y0, b.x0) == (max(0, b.y - halo), max(0, b.x - halo))
+        assert (b.y1, b.x1) == (min(h, b.y + b.h + halo), min(w, b.x + b.w + halo))
+        bh, bw = b.in_shape
+        assert 192 * 2 * (-(-bh // 16) * 16 + 2) * (-(-bw // 32) * 32 + 2) < 2 ** 31
+    assert bool((cover == 1).all())
+
+
+def test_plan_blocks_cfg4_beats_bands():
+    """cfg4 over 8 ranks: a 2 x 4 grid, one block per rank, at most 1112 x 1024 LR input — the
+    busiest rank runs 1.11x its ideal share against 1.24x for the 334-row bands."""
+    shards = tiler.plan_blocks(2160, 3840, 8, 32)
+    assert [len(s) for s in shards] == [1] * 8
+    shapes = {s[0].in_shape for s in shards}
+    assert shapes == {(1112, 992), (1112, 1024)}
+    band = tiler.plan_bands(2160, 3840, 8, 32)[0][0].in_shape
+    assert max(a * b for a, b in shapes) < 0.9 * band[0] * band[1]
+
+
+def test_blocks_single_rank_equals_whole_image_host_gather():
+    img = image(45, 61, seed=5)
+    full = box_up(img[None])[0]
+    up = tiler.TileUpscaler(box_up, S, window=16, halo=1, batch=1, device="cpu", shard="blocks", gather="host")
+    assert torch.equal(up(img), full)
+
+
 def test_runner_shape_check():
     up = tiler.TileUpscaler(lambda x: x, S, window=8, device="cpu")
     with pytest.raises(RuntimeError, match="runner returned"):
@@ -127,12 +162,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, shard="windows"):
+def _worker(rank, world, port, q, shard="windows", gather="device"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         img = image(45, 61, seed=11)
-        up = tiler.TileUpscaler(box_up, S, window=16, halo=2, batch=2, device="cpu", shard=shard)
+        batch = 2 if shard == "windows" else 1
+        up = tiler.TileUpscaler(box_up, S, window=16, halo=2, batch=batch, device="cpu", shard=shard,
+                                gather=gather)
         out = up(img, rank=rank, world=world)
         if rank == 0:
             q.put(out.numpy())  # by value: a shared-memory tensor handle can vanish when this rank exits
@@ -142,14 +179,16 @@ def _worker(rank, world, port, q, shard="windows"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("shard", ["windows", "bands"])
-def test_sharded_gloo_world2_matches_single(shard):
+@pytest.mark.parametrize("shard,gather", [("windows", "device"), ("bands", "device"), ("blocks", "device"),
+                                          ("blocks", "host")])
+def test_sharded_gloo_world2_matches_single(shard, gather):
     """2 ranks over gloo: the canvas rank 0 stitches equals the single-rank one (halo 2 >= the
-    operator's radius, so the bands deal gives the same whole-image result as windows)."""
+    operator's radius, so the bands / blocks deals give the same whole-image result as windows),
+    gathered point to point or through the shared host canvas."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shard)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shard, gather)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(2)]

@@ -10,12 +10,14 @@ Reports HR megapixels/s of the whole image (after one warm-up call that builds
 the plans), seconds per image, and peak device memory.
 
 --shard bands runs full-width bands (tiler.plan_bands) instead of rs.py's windows, on one GPU
-too (as few bands as the 2 GiB trunk-buffer window allows).
+too (as few bands as the 2 GiB trunk-buffer window allows); --shard blocks a 2-D grid of blocks
+(tiler.plan_blocks: 2 x 4 at 8 ranks).
 --sim-world N (one GPU, no torch.distributed): predicts the N-GPU wall time.  After the
 1-GPU run (t1, with the same --shard), every rank's share of an N-rank deal runs alone on this
 GPU, timed like the real run (same plans, median of --reps); the predicted N-GPU time is the
-slowest rank's, reported against t1 / N.  The gather of finished tiles to rank 0 is not
-included.
+slowest rank's, reported against t1 / N.  Each rank's time includes the hand-off of its finished
+tiles to the host: a device → pinned-host copy of its share of the canvas (1/N of it), as
+tiler's gather="host" does before the host assembly (reported apart, "assemble_s").
 usage: python tools/bench_still.py [--reps 3] [--batch 4] [--halo 32] [--shard bands] [--sim-world 8]
 """
 from __future__ import annotations
@@ -46,7 +48,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--shard", default="windows", choices=("windows", "bands"))
+    ap.add_argument("--shard", default="windows", choices=("windows", "bands", "blocks"))
     ap.add_argument("--sim-world", type=int, default=0)
     args = ap.parse_args()
     world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
@@ -116,27 +118,44 @@ def simulate(args, up, runner, img, t1, dev):
     N = args.sim_world
     shards = up.shards(img.shape[1], img.shape[2], N)
     ranks = []
+    s = up.scale
+    canvas = torch.zeros((3, img.shape[1] * s, img.shape[2] * s), dtype=torch.uint8)
     with torch.no_grad():
         for r in range(N):
-            up.run_tiles(img, shards[r])  # warm: builds this rank's plans
+            done = up.run_tiles(img, shards[r])  # warm: builds this rank's plans
             runner.verify()
-            ts = []
+            pins = {tt.index: torch.empty(done[tt.index].shape, dtype=torch.uint8, pin_memory=True)
+                    for tt in shards[r]}
+            ts, td, ta = [], [], []
             for _ in range(args.reps):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                up.run_tiles(img, shards[r])
+                done = up.run_tiles(img, shards[r])
                 runner.verify()
                 torch.cuda.synchronize()
-                ts.append(time.perf_counter() - t0)
+                t1r = time.perf_counter()
+                for tt in shards[r]:  # the hand-off: device → pinned host, 1/N of the canvas
+                    pins[tt.index].copy_(done[tt.index], non_blocking=True)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                for tt in shards[r]:  # host assembly into the canvas (reported apart)
+                    canvas[:, tt.y * s:(tt.y + tt.h) * s, tt.x * s:(tt.x + tt.w) * s] = pins[tt.index]
+                t3 = time.perf_counter()
+                ts.append(t2 - t0)
+                td.append(t2 - t1r)
+                ta.append(t3 - t2)
             shapes = sorted({tt.in_shape for tt in shards[r]})
-            ranks.append({"rank": r, "s": round(statistics.median(ts), 4), "tiles": len(shards[r]),
-                          "shapes": shapes, "run_px": sum(tt.cost for tt in shards[r])})
+            out_bytes = sum(pins[tt.index].numel() for tt in shards[r])
+            ranks.append({"rank": r, "s": round(statistics.median(ts), 4), "d2h_s": round(statistics.median(td), 5),
+                          "assemble_s": round(statistics.median(ta), 5), "out_mb": round(out_bytes / 1e6, 1),
+                          "tiles": len(shards[r]), "shapes": shapes, "run_px": sum(tt.cost for tt in shards[r])})
             print(json.dumps({"sim_rank": ranks[-1]}), flush=True)
     mx = max(x["s"] for x in ranks)
     return {"sim_world": N, "shard": args.shard, "sim_ranks": ranks, "sim_max_rank_s": mx,
             "sim_t1_over_n_s": round(t1 / N, 4), "sim_ratio": round(mx / (t1 / N), 3),
             "sim_value_mpix_s": round(args.height * args.width * 16 / mx / 1e6, 1),
-            "sim_note": "per-rank shares run alone on one GPU; gather to rank 0 excluded"}
+            "sim_note": "per-rank shares run alone on one GPU; each rank's time includes the device -> "
+                        "pinned-host copy of its share of the canvas (d2h_s); host assembly (assemble_s) apart"}
 
 
 if __name__ == "__main__":
