@@ -208,6 +208,9 @@ struct TK {
     static_assert(LDS <= 163840, "LDS budget");
     static constexpr int BPC = 163840 / LDS < 2 ? 163840 / LDS : 2;  // workgroups per CU
     static constexpr int WPS = BPC * WM / 4;                          // waves per SIMD
+    // fragment sets: 2 (the next dx step's fragments read during this step's MFMAs) or, at 4 waves
+    // per SIMD (128 VGPRs), 1 — each step reads its own, the SIMD's other waves cover the latency
+    static constexpr int NSET = WPS >= 4 ? 1 : 2;
 };
 
 // Where the chunks of one (layer, tile) item come from (LDS-DMA through buffer resources:
@@ -308,6 +311,17 @@ __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src&
         return 0;
     }
 #endif
+    if constexpr (K::NSET == 1) {
+        // the 128-VGPR form: the per-lane halo offsets rebuilt from an opaque lane id per chunk
+        // (kept live they spilled, and a scratch reload's vmcnt wait would drain the ring's DMA)
+        int ln = threadIdx.x & 63;
+        asm volatile("" : "+v"(ln));
+        uint32_t ho[K::HPW];
+#pragma unroll
+        for (int k = 0; k < K::HPW; ++k) ho[k] = halo_piece_off<K::HQ>(wave_id() + K::WM * k, ln, c.wp);
+        return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF, K::HP>(ho, c.pstride, c.abl, s, chunk, slot,
+                                                                          with_bias, bslot);
+    }
     return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF, K::HP>(c.hoff, c.pstride, c.abl, s, chunk, slot,
                                                                       with_bias, bslot);
 }
@@ -561,14 +575,27 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                 }
             }
             const char* sb = smem + slot * K::SLOT;
-            bf16x8 fb[2][TN][NF], fa[2][NA];
+            constexpr int NSET = K::NSET;
+            // the 1-set (128-VGPR) form rebuilds its fragment addresses from an opaque lane id at
+            // each chunk: kept live across the chunks, they were what it spilled
+            uint32_t aw = a_w, ah[3] = {a_h[0], a_h[1], a_h[2]};
+            if constexpr (NSET == 1) {
+                int ln = threadIdx.x & 63;
+                asm volatile("" : "+v"(ln));
+                const int q31 = ln & 31, qh = ln >> 5;
+                aw = (uint32_t)(K::HP * 1024 + (2 * q31 + (qh ^ ((q31 >> 3) & 1))) * 16);
+    #pragma unroll
+                for (int dx = 0; dx < 3; ++dx)
+                    ah[dx] = (uint32_t)((wave * R * tk::HC + q31 + dx) * 32 + 16 * (qh ^ (((q31 + dx) >> 3) & 1)));
+            }
+            bf16x8 fb[NSET][TN][NF], fa[NSET][NA];
             auto read_one = [&](int dx, int idx, int set) {
                 if (idx < TN * NF) {
                     const int dyi = idx / NF, f = idx % NF;
-                    fb[set][dyi][f] = lds_read16(sb + a_w + ((dyi * 3 + dx) * CT * 2 + f * 64) * 16);
+                    fb[set][dyi][f] = lds_read16(sb + aw + ((dyi * 3 + dx) * CT * 2 + f * 64) * 16);
                 } else {
                     const int ia = idx - TN * NF;
-                    fa[set][ia] = lds_read16(sb + a_h[dx] + ia * tk::HC * 32);
+                    fa[set][ia] = lds_read16(sb + ah[dx] + ia * tk::HC * 32);
                 }
             };
             auto read_fb = [&](int dx, int dyi, int set) {
@@ -578,6 +605,13 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
             // step 0's fragments in order of first use (kernel-row-major MFMA order below); with
             // ISR_TRUNK_REFILL_FIRST the refill's LDS-DMA is issued before them instead of after
             auto read_step0 = [&]() {
+                if constexpr (K::NSET == 1) {  // lazy: kernel row 0's weights and its R input rows
+                    read_fb(0, 0, 0);
+    #pragma unroll
+                    for (int ia = 0; ia < R; ++ia) read_one(0, TN * NF + ia, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    return;
+                }
                 read_fb(0, 0, 0);
     #pragma unroll
                 for (int ia = 0; ia < R; ++ia) read_one(0, TN * NF + ia, 0);
@@ -645,9 +679,26 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
             // input row ia right after the current one's last use. ----
     #pragma unroll
             for (int stp = 0; stp < 3; ++stp) {
-                const int cur = stp & 1;
+                const int cur = NSET == 2 ? (stp & 1) : 0;
+                if constexpr (NSET == 1) {
+                    if (stp > 0) {  // lazy: kernel row 0's weights and the first R input rows
+                        read_fb(stp, 0, 0);
+    #pragma unroll
+                        for (int ia = 0; ia < R; ++ia) read_one(stp, TN * NF + ia, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
     #pragma unroll
                 for (int dyi = 0; dyi < TN; ++dyi) {
+                    if constexpr (NSET == 1) {
+                        // the next kernel row's weights and its one new input row, one row ahead:
+                        // at most two kernel rows' fragments are live (the 128-VGPR budget)
+                        if (dyi + 1 < TN) {
+                            read_fb(stp, dyi + 1, 0);
+                            read_one(stp, TN * NF + dyi + R, 0);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    }
     #pragma unroll
                     for (int r = 0; r < R; ++r) {
     #pragma unroll
@@ -656,16 +707,17 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                             // residual fold: + x/s1 on the centre pixels of row r (dx = 1, dy = 1),
                             // between the row's dy = 1 and dy = 2 contributions (chunk FC, compile-time)
                             if (dyi == 1 && stp == 1) {
-                                const bf16x8 a = fold_a_bits(idv, FC & 1);
+                                const bf16x8 a = fold_a_bits<K::NSET == 1>(idv, FC & 1);
                                 acc[r][FC >> 1] = mfma32(a, fa[cur][r + 1], acc[r][FC >> 1]);
                             }
                         }
                         // input row ia = r + dyi is last used here when dyi == min(2, ia)
-                        if (stp + 1 < 3 && (dyi == 2 || r == 0)) read_one(stp + 1, TN * NF + r + dyi, cur ^ 1);
+                        if (NSET == 2 && stp + 1 < 3 && (dyi == 2 || r == 0))
+                            read_one(stp + 1, TN * NF + r + dyi, cur ^ 1);
                         if (stp == kTrunkInterleaveStep && rf.on) rf_n += refill_piece<K>(c, rf, dyi * R + r);
                         __builtin_amdgcn_sched_barrier(0);
                     }
-                    if (stp + 1 < 3) {
+                    if (NSET == 2 && stp + 1 < 3) {
                         read_fb(stp + 1, dyi, cur ^ 1);
                         __builtin_amdgcn_sched_barrier(0);
                     }
@@ -816,7 +868,7 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
     {
         const int wave = wave_id(), lane = threadIdx.x & 63;
 #pragma unroll
-        for (int k = 0; k < K::HPW; ++k) c.hoff[k] = halo_piece_off<K::HQ>(wave + K::WM * k, lane, c.wp);
+        for (int k = 0; k < K::HPW; ++k) c.hoff[k] = K::NSET == 1 ? 0u : halo_piece_off<K::HQ>(wave + K::WM * k, lane, c.wp);
     }
     const int G = gridDim.x, b = blockIdx.x;
 #if ISR_TRUNK_PRIO == 2
@@ -922,6 +974,9 @@ using TK_DEEP = TK<8, 2, 4>;   // one 8-wave workgroup per CU, 3 chunks in fligh
 // 32x32 tiles: one 8-wave workgroup per CU (4 rows per wave, as the pair form), the chunk's
 // weights staged once per CU instead of twice and a (34x34)/(32x32) halo instead of (18x34)/(16x32)
 using TK_T32 = TK<8, 4, 2, 32>;
+// the pair form's tile, ring and two workgroups per CU with 8 waves each (2 rows per wave): 4 waves
+// per SIMD at 128 VGPRs (one fragment set), and each wave issues half the refill pieces
+using TK_QUAD = TK<8, 2, 2>;
 
 int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_deep.hip
 int trunk_deep_knobs_set(const int* k);
@@ -929,6 +984,7 @@ int trunk_deep_knobs_set(const int* k);
 int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
     if (form == 3) return trunk_deep_launch(cd, s);
     if (form == 2) return trunk_launch_k<TK_T32>(cd, s);
+    if (form == 4) return trunk_launch_k<TK_QUAD>(cd, s);
     return form == 1 ? trunk_launch_k<TK_DEEP>(cd, s) : trunk_launch_k<TK_PAIR>(cd, s);
 }
 

@@ -140,8 +140,12 @@ template <int V> struct TIC { static constexpr int value = V; };
 
 // A operand of the residual fold: (1/s1) I on couts [16 h16, 16 h16 + 16) of a 32-cout
 // fragment (lane l supplies A[l & 31][8 (l >> 5) .. + 8]); conv3x3.hip builds the same.
+template <bool FRESH = false>
 __device__ __forceinline__ bf16x8 fold_a_bits(uint32_t idv, int h16) {
-    const int lane = threadIdx.x & 63;
+    int lane = threadIdx.x & 63;
+    // FRESH: an opaque copy of the lane id, so the operand is rebuilt at each use (a few VALU ops
+    // in the MFMA shadow) instead of being hoisted and kept live in 8 VGPRs across the chunks
+    if constexpr (FRESH) asm volatile("" : "+v"(lane));
     const int j = (lane & 31) - 16 * h16 - 8 * (lane >> 5);
     typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
     u32x4 r;

@@ -446,7 +446,8 @@ CHAIN_DEFAULT = _os.environ.get("ISR_CHAIN", "1") == "1"
 # invalidates L1, so it adds nothing to them and costs ~1 ms per forward on the trunk kernel
 # (per-wave fences).  Both modes are bitwise-tested (tests/test_gpu_chain.py).
 CHAIN_ACQUIRE = _os.environ.get("ISR_CHAIN_ACQUIRE", "0") == "1"
-# isr_conv_chain_variant: 0 = trunk.hip (production), 1 = the round-2 per-tile chain kernel
+# isr_conv_chain_variant: 0 = trunk.hip (production), 1 = the round-2 per-tile chain kernel, 2-5 the
+# A/B forms documented at isr_conv_chain_variant in include/isr.h
 CHAIN_VARIANT = int(_os.environ.get("ISR_CHAIN_VARIANT", "0"))
 
 

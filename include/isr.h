@@ -387,7 +387,9 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
  * tiles, one 8-wave workgroup per CU (4 rows per wave; needs ha % 32 == 0); 4 = trunk_deep.hip:
  * 32x32 tiles, one 8-wave workgroup per CU, split halo (3 slots) / weight (2 slots) rings, the
  * chunk barrier before the last MFMA step with the next chunk's fragments read behind it, LDS-DMA
- * spread over the MFMA stream, neighbourhood polls by LDS-DMA (needs ha % 32 == 0). */
+ * spread over the MFMA stream, neighbourhood polls by LDS-DMA (needs ha % 32 == 0); 5 = trunk.hip's
+ * pair tile and ring with two 8-wave workgroups per CU (2 rows per wave, 4 waves per SIMD at
+ * 128 VGPRs: one fragment set read a kernel row ahead, half the refill pieces per wave). */
 int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
 /* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
  * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,
