@@ -77,7 +77,7 @@ def parse():
     ap.add_argument("--scale", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r03")
+    ap.add_argument("--round", default="r04")
     ap.add_argument("--no-graph", action="store_true", help="eager launch loop instead of the HIP graph")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N>1 (nccl = RCCL)")
     ap.add_argument("--streams", type=int, default=None,
