@@ -191,9 +191,13 @@ __device__ __forceinline__ void glds4(const void* gsrc, void* lds) {
 // K-chunks in flight).  <4, 4, 2>: two 4-wave workgroups per CU, one chunk in flight (the
 // round-3 first form); <8, 2, 4>: one 8-wave workgroup per CU, three chunks in flight, two tiles
 // of independent images interleaved per layer.
-template <int WM_, int R_, int NST_, int TH_ = 16>
+template <int WM_, int R_, int NST_, int TH_ = 16, int XM_ = 0>
 struct TK {
     static constexpr int WM = WM_, R = R_, NST = NST_;
+    // XM = 1: XCD-aware tile deal — workgroup b (dispatched round-robin to XCD b % 8) works as
+    // virtual workgroup xcd_remap(b), so each XCD streams a contiguous range of tiles and a tile's
+    // halo neighbours were written through the same XCD's L2
+    static constexpr int XM = XM_;
     static constexpr int NT = 64 * WM;
     static constexpr int TH = TH_;                        // tile rows (x 32 columns)
     static constexpr int HQ = (TH + 2) * tk::HC;          // halo pixels of a chunk
@@ -870,7 +874,7 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
 #pragma unroll
         for (int k = 0; k < K::HPW; ++k) c.hoff[k] = K::NSET == 1 ? 0u : halo_piece_off<K::HQ>(wave + K::WM * k, lane, c.wp);
     }
-    const int G = gridDim.x, b = blockIdx.x;
+    const int G = gridDim.x, b = K::XM ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
 #if ISR_TRUNK_PRIO == 2
     // tuning A/B: the later-dispatched half of the grid (a CU's second workgroup) at priority 1
     if (__builtin_amdgcn_readfirstlane(b) >= G / 2) __builtin_amdgcn_s_setprio(1);
@@ -977,6 +981,7 @@ using TK_T32 = TK<8, 4, 2, 32>;
 // the pair form's tile, ring and two workgroups per CU with 8 waves each (2 rows per wave): 4 waves
 // per SIMD at 128 VGPRs (one fragment set), and each wave issues half the refill pieces
 using TK_QUAD = TK<8, 2, 2>;
+using TK_PAIR_X = TK<4, 4, 2, 16, 1>;  // the pair form with the XCD-aware tile deal
 
 int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_deep.hip
 int trunk_deep_knobs_set(const int* k);
@@ -985,6 +990,7 @@ int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
     if (form == 3) return trunk_deep_launch(cd, s);
     if (form == 2) return trunk_launch_k<TK_T32>(cd, s);
     if (form == 4) return trunk_launch_k<TK_QUAD>(cd, s);
+    if (form == 5) return trunk_launch_k<TK_PAIR_X>(cd, s);
     return form == 1 ? trunk_launch_k<TK_DEEP>(cd, s) : trunk_launch_k<TK_PAIR>(cd, s);
 }
 
