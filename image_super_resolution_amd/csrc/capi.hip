@@ -43,7 +43,7 @@ int maxpool2_dispatch(const isr_pool_desc* d, int backward, hipStream_t s);
 size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d, int variant);
 size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
 int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
-int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s);
+int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s, int parts);
 int mt_adam_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, const isr_adam_args* a,
                      const float* scale, const uint32_t* guard, hipStream_t s);
 int mt_sumsq_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, float* partial, hipStream_t s);
@@ -383,13 +383,13 @@ size_t isr_wgrad3x3_workspace_bytes(const isr_wgrad_desc* d) {
     return isr::wgrad3x3_workspace_bytes(d, 0);
 }
 
-int isr_wgrad3x3_variant(const isr_wgrad_desc* d, int32_t variant, void* workspace, size_t ws_bytes,
-                         isr_stream_t s) {
+static int wgrad3x3_parts(const isr_wgrad_desc* d, int32_t variant, void* workspace, size_t ws_bytes,
+                          isr_stream_t s, int parts) {
     int rc = wgrad_validate(d);
     if (rc != ISR_OK) return rc;
     if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null workspace");
     if (variant < 0 || variant > 14) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: no variant %d", variant);
-    rc = isr::wgrad3x3_dispatch(d, variant, workspace, ws_bytes, (hipStream_t)s);
+    rc = isr::wgrad3x3_dispatch(d, variant, workspace, ws_bytes, (hipStream_t)s, parts);
     if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: workspace of %zu bytes is smaller than %zu", ws_bytes,
                               isr::wgrad3x3_workspace_bytes(d, variant));
     if (rc == -2)
@@ -398,8 +398,21 @@ int isr_wgrad3x3_variant(const isr_wgrad_desc* d, int32_t variant, void* workspa
     return launched(rc, "wgrad3x3");
 }
 
+int isr_wgrad3x3_variant(const isr_wgrad_desc* d, int32_t variant, void* workspace, size_t ws_bytes,
+                         isr_stream_t s) {
+    return wgrad3x3_parts(d, variant, workspace, ws_bytes, s, 3);
+}
+
 int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
-    return isr_wgrad3x3_variant(d, 0, workspace, ws_bytes, s);
+    return wgrad3x3_parts(d, 0, workspace, ws_bytes, s, 3);
+}
+
+int isr_wgrad3x3_partials(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
+    return wgrad3x3_parts(d, 0, workspace, ws_bytes, s, 1);
+}
+
+int isr_wgrad3x3_reduce(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
+    return wgrad3x3_parts(d, 0, workspace, ws_bytes, s, 2);
 }
 
 size_t isr_wgrad3x3_variant_workspace_bytes(const isr_wgrad_desc* d, int32_t variant) {

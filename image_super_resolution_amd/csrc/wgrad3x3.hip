@@ -23,6 +23,7 @@
 // reduces over splits, applies `scale`, and writes dW in the reference OIHW
 // layout (and un-permutes the PixelShuffle channel order for g_sub2).
 #include "isr_common.h"
+#include <cstdlib>
 
 namespace isr {
 
@@ -403,19 +404,31 @@ static void wgrad_geometry(const isr_wgrad_desc* d, int* tiles, int* splits) {
     *splits = wgrad_splits(d, *tiles, pairs, target, C::KW == 2 && pairs <= 16 ? 64 : 1);
 }
 
+// parts: 1 = the split-K partials, 2 = their reduction into dW / db, 3 = both (in stream order)
 template <class C>
-static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s) {
+static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipStream_t s, int parts = 3) {
     if (d->ha % C::TY || d->cout % C::CO_T || d->cin % C::CI_T) return -2;
     WgradArgs a;
     a.d = *d;
     wgrad_geometry<C>(d, &a.tiles, &a.splits);
     if (ws_bytes < ((size_t)a.splits * 9 * d->cout * d->cin + (size_t)a.splits * d->cout) * 4) return -3;
     a.ws = (float*)ws;
-    auto kern = wgrad3x3_kernel<C>;
-    lds_limit((const void*)kern, C::LDS);
-    const int blocks = a.splits * (d->cout / C::CO_T) * (d->cin / C::CI_T);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, a);
-    if (hipGetLastError() != hipSuccess) return -1;
+#ifdef ISR_TUNING
+    // timing probes of the training step (outputs wrong): no weight gradients at all / no reduce
+    static const bool skip_all = getenv("ISR_WGRAD_SKIP") != nullptr, skip_red = getenv("ISR_WGRAD_NO_REDUCE") != nullptr;
+    if (skip_all) return 0;
+#endif
+    if (parts & 1) {
+        auto kern = wgrad3x3_kernel<C>;
+        lds_limit((const void*)kern, C::LDS);
+        const int blocks = a.splits * (d->cout / C::CO_T) * (d->cin / C::CI_T);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(C::NT), C::LDS, s, a);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    if (!(parts & 2)) return 0;
+#ifdef ISR_TUNING
+    if (skip_red) return 0;
+#endif
     // the transposing reduce has one block per (co, 32 ci): it pays only for large weights (the
     // discriminator's phase-expanded 128..512 x 512..2048); the generator's <= 256 x 192 keep
     // the column-wise reduce (more blocks: 30 vs 48 us per wgrad at 32 x 64)
@@ -526,8 +539,8 @@ size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d, int variant) {
     });
 }
 
-int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s) {
-    return wgrad_pick(d, variant, [&](auto c) { return launch_wgrad<decltype(c)>(d, ws, ws_bytes, s); });
+int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s, int parts) {
+    return wgrad_pick(d, variant, [&](auto c) { return launch_wgrad<decltype(c)>(d, ws, ws_bytes, s, parts); });
 }
 
 }  // namespace isr

@@ -420,6 +420,17 @@ class GeneratorTrainPlan:
         self.ws_side = torch.empty(nbytes, dtype=torch.uint8, device=dev) if self.gather else None
         self.side = (torch.cuda.Stream(dev) if self.gather and _os.environ.get("ISR_TRAIN_SIDE", "1") == "1"
                      else None)
+        # the side stream's split-K reductions run on a third stream: the side stream chains only
+        # the weight-gradient kernels (each reduce had sat between two of them: 3.3 ms per cfg3
+        # step, tools/r04_train_probe.sh), over a ring of RED_RING workspaces — a slot is reused
+        # once the reduce that read it has finished
+        self.red = None
+        if self.side is not None and _os.environ.get("ISR_TRAIN_RED_STREAM", "1") == "1":
+            self.red = torch.cuda.Stream(dev)
+            self.ws_ring = [self.ws_side] + [torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                                             for _ in range(RED_RING - 1)]
+            self.ev_part = [torch.cuda.Event() for _ in range(RED_RING)]
+            self.ev_red = [torch.cuda.Event() for _ in range(RED_RING)]
         self.events = {}
         # gradient offsets per conv: (w, b or None, bn weight or None, bn bias or None)
         self._conv_goff = []
@@ -493,11 +504,17 @@ class GeneratorTrainPlan:
             sst = ctypes.c_void_p(self.side.cuda_stream)
         group = self.gen.__dict__.get("_isr_grad_group")
         ddp = _Buckets(self, grads, group, main) if group is not None else None
+        red = self.red
+        if red is not None:
+            rst = ctypes.c_void_p(red.cuda_stream)
+            red_used = [False] * RED_RING
+            nside = 0
+        side_done = red if red is not None else self.side  # where a side-produced segment completes
         for e in self.bwd_launches:
             kind, d = e[0], e[1]
             if kind == "ready":
                 if ddp is not None:
-                    ddp.ready(d, self.side if (e[2] and self.side is not None) else main)
+                    ddp.ready(d, side_done if (e[2] and self.side is not None) else main)
                 continue
             if kind in ("evrec", "evwait") and self.side is None:
                 continue
@@ -524,7 +541,20 @@ class GeneratorTrainPlan:
                 wo, bo = self._conv_goff[e[2]][:2]
                 d.dw = gbase + 4 * wo
                 d.db = gbase + 4 * bo if bo is not None else None
-                if kind == "wg3" and e[3] and self.side is not None:
+                if kind == "wg3" and e[3] and red is not None:
+                    k = nside % RED_RING
+                    nside += 1
+                    wsk = self.ws_ring[k]
+                    if red_used[k]:
+                        self.side.wait_event(self.ev_red[k])  # the slot's previous reduce has read it
+                    rc = lib.isr_wgrad3x3_partials(byref(d), wsk.data_ptr(), wsk.numel(), sst)
+                    if rc == 0:
+                        self.ev_part[k].record(self.side)
+                        red.wait_event(self.ev_part[k])
+                        rc = lib.isr_wgrad3x3_reduce(byref(d), wsk.data_ptr(), wsk.numel(), rst)
+                        self.ev_red[k].record(red)
+                        red_used[k] = True
+                elif kind == "wg3" and e[3] and self.side is not None:
                     rc = lib.isr_wgrad3x3(byref(d), self.ws_side.data_ptr(), self.ws_side.numel(), sst)
                 else:
                     rc = (lib.isr_wgrad3x3 if kind == "wg3" else lib.isr_wgrad9x9)(byref(d), ws, wsn, st)
@@ -536,12 +566,18 @@ class GeneratorTrainPlan:
                 ops.check(rc, f"train backward ({kind})")
         if side_used:
             main.wait_stream(self.side)
+            if red is not None:
+                main.wait_stream(red)
         if ddp is not None:
             ddp.finish()  # the main stream waits for every bucket, then the mean
         out = []
         for p, off in zip(self._params, self._goff):
             out.append(grads[off:off + p.numel()].view(p.shape))
         return out
+
+
+# workspaces in the ring of the side stream's split-K partials (train plan with a reduce stream)
+RED_RING = 4
 
 
 # DDP-style gradient buckets: consecutive backward segments are merged until a bucket holds at

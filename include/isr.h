@@ -178,6 +178,12 @@ int isr_wgrad9x9(const isr_wgrad9_desc* d, void* workspace, size_t ws_bytes, isr
 
 size_t isr_wgrad3x3_workspace_bytes(const isr_wgrad_desc* d);
 int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
+/* isr_wgrad3x3 in two launches: the split-K partial sums into `workspace`, then their reduction
+ * into dw / db (same descriptor and workspace; the caller orders the second after the first, on
+ * another stream too, and keeps the workspace untouched in between).  Lets a caller take the
+ * reductions off the stream that chains the weight-gradient kernels (train_engine.py). */
+int isr_wgrad3x3_partials(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
+int isr_wgrad3x3_reduce(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
 /* Tuning: the same computation by an explicit kernel variant (0 = production;
  * 1..4 = stage-geometry alternatives, see wgrad3x3.hip), with its own workspace size. */
 size_t isr_wgrad3x3_variant_workspace_bytes(const isr_wgrad_desc* d, int32_t variant);

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Split-K reductions of the side stream's weight gradients on a third stream: training parity
+# tests, then a same-box A/B of the cfg3 step (alternating processes).
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/r04
+mkdir -p $O
+step() { local t=$1; shift; local name=$1; shift; echo "== $name"; timeout -k 10 $t "$@" > $O/$name.out 2> $O/$name.err; local rc=$?; echo "rc=$rc"; tail -3 $O/$name.out; return $rc; }
+PT="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
+step 500 rs_tests $PT -s tests/test_gpu_train.py tests/test_gpu_train_cfg3.py tests/test_gpu_dist_train.py tests/test_gpu_chain.py &&
+ISR_TRAIN_RED_STREAM=1 step 200 rs_on1 python -u tools/bench_train.py --steps 10 --warmup 3 &&
+ISR_TRAIN_RED_STREAM=0 step 200 rs_off1 python -u tools/bench_train.py --steps 10 --warmup 3 &&
+ISR_TRAIN_RED_STREAM=1 step 200 rs_on2 python -u tools/bench_train.py --steps 10 --warmup 3 &&
+ISR_TRAIN_RED_STREAM=0 step 200 rs_off2 python -u tools/bench_train.py --steps 10 --warmup 3
