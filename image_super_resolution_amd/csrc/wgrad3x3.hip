@@ -329,8 +329,13 @@ __global__ __launch_bounds__(128) void wgrad_reduce_t_kernel(WgradArgs a) {
 // first form, 4 slices x 64 columns, launched 181 blocks for a growth conv's 46 K weights —
 // under one per CU — and each thread walked S/4 = 16..64 dependent rows: ~20 us per reduce,
 // latency-bound, on the side stream beside the RDB gather convs.)
-constexpr int RED_SL = 16, RED_COLS = 16;
+// RED_SL split-slices x RED_COLS 16-byte columns per 256-thread block: every thread streams
+// S / RED_SL rows of one column with all its loads in flight (UNR-deep unroll), the slices are
+// summed through LDS in slice order.  Production <16, 16, 4>; the tuning build picks others
+// with ISR_WGRAD_RED (timing A/B of the cfg3 step).
+template <int RED_SL, int RED_COLS, int UNR>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
+    static_assert(RED_SL * RED_COLS == 256, "one 256-thread block");
     __shared__ f32x4 red[RED_SL][RED_COLS];
     const isr_wgrad_desc& d = a.d;
     const size_t per = (size_t)9 * d.cout * d.cin;
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (col < nv) {
         const f32x4* src = reinterpret_cast<const f32x4*>(a.ws) + col;
-#pragma unroll 4
+#pragma unroll UNR
         for (int sp = slice; sp < a.splits; sp += RED_SL) acc += src[(size_t)sp * (row / 4)];
     }
     red[slice][lc] = acc;
@@ -366,6 +371,13 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
             d.db[co] = acc[e] * d.scale;
         }
     }
+}
+
+template <int SL, int COLS, int UNR>
+static void launch_reduce(const WgradArgs& a, hipStream_t s) {
+    const size_t nv = ((size_t)9 * a.d.cout * a.d.cin + a.d.cout) / 4;
+    hipLaunchKernelGGL((wgrad_reduce_kernel<SL, COLS, UNR>), dim3((unsigned)((nv + COLS - 1) / COLS)), dim3(256), 0, s,
+                       a);
 }
 
 // Variants (isr_wgrad3x3_variant; tools/tune_wgrad.py).  TY = pixel rows per
@@ -436,8 +448,17 @@ static int launch_wgrad(const isr_wgrad_desc* d, void* ws, size_t ws_bytes, hipS
         hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)(d->cout * (d->cin / 32))), dim3(128), 0, s, a);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    const size_t nv = ((size_t)9 * d->cout * d->cin + d->cout) / 4;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nv + RED_COLS - 1) / RED_COLS)), dim3(256), 0, s, a);
+#ifdef ISR_TUNING
+    static const int red_v = getenv("ISR_WGRAD_RED") ? atoi(getenv("ISR_WGRAD_RED")) : 0;
+    switch (red_v) {
+        case 1: launch_reduce<32, 8, 8>(a, s); return hipGetLastError() == hipSuccess ? 0 : -1;
+        case 2: launch_reduce<8, 32, 8>(a, s); return hipGetLastError() == hipSuccess ? 0 : -1;
+        case 3: launch_reduce<16, 16, 8>(a, s); return hipGetLastError() == hipSuccess ? 0 : -1;
+        case 4: launch_reduce<64, 4, 4>(a, s); return hipGetLastError() == hipSuccess ? 0 : -1;
+        default: break;
+    }
+#endif
+    launch_reduce<16, 16, 4>(a, s);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

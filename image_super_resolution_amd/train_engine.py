@@ -420,12 +420,15 @@ class GeneratorTrainPlan:
         self.ws_side = torch.empty(nbytes, dtype=torch.uint8, device=dev) if self.gather else None
         self.side = (torch.cuda.Stream(dev) if self.gather and _os.environ.get("ISR_TRAIN_SIDE", "1") == "1"
                      else None)
-        # the side stream's split-K reductions run on a third stream: the side stream chains only
-        # the weight-gradient kernels (each reduce had sat between two of them: 3.3 ms per cfg3
-        # step, tools/r04_train_probe.sh), over a ring of RED_RING workspaces — a slot is reused
-        # once the reduce that read it has finished
+        # A/B option (ISR_TRAIN_RED_STREAM=1, off): the side stream's split-K reductions on a third
+        # stream over a ring of RED_RING workspaces (a slot is reused once the reduce that read it
+        # has finished), so the side stream chains only the weight-gradient kernels.  Skipping the
+        # reductions altogether saves 3.3 ms per cfg3 step (tuning probe, tools/r04_train_probe.sh),
+        # but moving them off the chain loses 1.2 ms (51.7 / 51.8 vs 50.5 / 50.6 ms, alternating
+        # processes, profiles/r04_train_red_stream_ab.jsonl): their cost is the partials' traffic,
+        # not their place in the chain
         self.red = None
-        if self.side is not None and _os.environ.get("ISR_TRAIN_RED_STREAM", "1") == "1":
+        if self.side is not None and _os.environ.get("ISR_TRAIN_RED_STREAM", "0") == "1":
             self.red = torch.cuda.Stream(dev)
             self.ws_ring = [self.ws_side] + [torch.empty(nbytes, dtype=torch.uint8, device=dev)
                                              for _ in range(RED_RING - 1)]
