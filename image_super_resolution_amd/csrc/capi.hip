@@ -44,6 +44,8 @@ size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d, int variant);
 size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
 int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
 int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s, int parts);
+size_t wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* ds, int n);
+int wgrad3x3_group_dispatch(const isr_wgrad_desc* ds, int n, void* ws, size_t ws_bytes, hipStream_t s);
 int mt_adam_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, const isr_adam_args* a,
                      const float* scale, const uint32_t* guard, hipStream_t s);
 int mt_sumsq_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, float* partial, hipStream_t s);
@@ -405,6 +407,35 @@ int isr_wgrad3x3_variant(const isr_wgrad_desc* d, int32_t variant, void* workspa
 
 int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
     return wgrad3x3_parts(d, 0, workspace, ws_bytes, s, 3);
+}
+
+static int wgrad_group_validate(const isr_wgrad_desc* ds, int32_t n) {
+    if (!ds || n < 1 || n > 5) return fail(ISR_ERR_BAD_DESC, "wgrad3x3 group: null descriptors or n not in [1, 5]");
+    for (int t = 0; t < n; ++t) {
+        const int rc = wgrad_validate(&ds[t]);
+        if (rc != ISR_OK) return rc;
+        if (ds[t].g_sub2 || ds[t].x_sub2 || ds[t].taps || ds[t].n != ds[0].n || ds[t].ha != ds[0].ha ||
+            ds[t].wa != ds[0].wa)
+            return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3 group: member %d is not a plain 3x3 conv on the first "
+                        "member's grid", t);
+    }
+    return ISR_OK;
+}
+
+size_t isr_wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* descs, int32_t n) {
+    if (wgrad_group_validate(descs, n) != ISR_OK) return 0;
+    return isr::wgrad3x3_group_workspace_bytes(descs, n);
+}
+
+int isr_wgrad3x3_group(const isr_wgrad_desc* descs, int32_t n, void* workspace, size_t ws_bytes, isr_stream_t s) {
+    int rc = wgrad_group_validate(descs, n);
+    if (rc != ISR_OK) return rc;
+    if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad3x3 group: null workspace");
+    rc = isr::wgrad3x3_group_dispatch(descs, n, workspace, ws_bytes, (hipStream_t)s);
+    if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad3x3 group: workspace of %zu bytes is smaller than %zu", ws_bytes,
+                              isr::wgrad3x3_group_workspace_bytes(descs, n));
+    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3 group: a member's cout / cin / ha does not fit the tile");
+    return launched(rc, "wgrad3x3 group");
 }
 
 int isr_wgrad3x3_partials(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {

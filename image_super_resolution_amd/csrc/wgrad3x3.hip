@@ -79,17 +79,16 @@ struct WgradArgs {
     int splits, tiles;
 };
 
+// One block's work: (ci tile, co tile, split) = the block index b within its conv.
 template <class C>
-__global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
+__device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, int splits, int tiles, int b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const isr_wgrad_desc& d = a.d;
     constexpr int NCO = C::NCO, NCI = C::NCI, TY = C::TY;
     const int ncot = d.cout / C::CO_T, ncit = d.cin / C::CI_T;
-    int b = xcd_remap(blockIdx.x, gridDim.x);
     const int cit = b % ncit; b /= ncit;
     const int cot = b % ncot; b /= ncot;
     const int split = b;
-    const int t0 = (int)((long)split * a.tiles / a.splits), t1 = (int)((long)(split + 1) * a.tiles / a.splits);
+    const int t0 = (int)((long)split * tiles / splits), t1 = (int)((long)(split + 1) * tiles / splits);
     const int wave = wave_id();
     const int dy = wave % C::TN, kh = (wave / C::TN) % C::KW;  // kernel row, K-share of this wave
     const int cw = wave / (C::TN * C::KW);                       // ci-tile group of this wave
@@ -259,7 +258,7 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
 
     // ---- partial sums: ws[split][tap][co][ci], D[co = (g&3)+8(g>>2)+4h][ci = l31]
     const int l31 = lane & 31;
-    float* wsp = a.ws + (size_t)split * (9 * d.cout * d.cin + d.cout);
+    float* wsp = ws + (size_t)split * (9 * d.cout * d.cin + d.cout);
 #pragma unroll
     for (int dx = 0; dx < C::TN; ++dx) {
         float* wt = wsp + (size_t)(dy * 3 + dx) * d.cout * d.cin;
@@ -282,6 +281,39 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
             if (hh == 0) bp[cot * C::CO_T + f * 32 + (gi * 16 + (lane & 15))] = v;
         }
     }
+}
+
+template <class C>
+__global__ __launch_bounds__(C::NT) void wgrad3x3_kernel(WgradArgs a) {
+    wgrad_body<C>(a.d, a.ws, a.splits, a.tiles, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// Several weight gradients over the same pixel grid in ONE launch (the 5 convs of an RDB read
+// one dense buffer and one gradient buffer): the blocks of conv t are [start[t], start[t+1]),
+// each conv's partials in its own workspace range.  With all the convs' (co, ci) tile pairs in
+// one grid, a split count ~5x smaller fills the chip — each block walks ~5x more pixel tiles and
+// the split-K partials written and reduced shrink by the same factor.
+constexpr int WG_GROUP_MAX = 5;
+struct WgradGroupArgs {
+    isr_wgrad_desc d[WG_GROUP_MAX];
+    float* ws[WG_GROUP_MAX];
+    int start[WG_GROUP_MAX + 1];   // wgrad blocks
+    int rstart[WG_GROUP_MAX + 1];  // reduce blocks
+    int n, splits, tiles;
+};
+
+__device__ __forceinline__ int group_member(const WgradGroupArgs& g, const int* start, int b) {
+    int t = 0;
+#pragma unroll
+    for (int k = 1; k < WG_GROUP_MAX; ++k) t += (k < g.n && b >= start[k]) ? 1 : 0;
+    return t;
+}
+
+template <class C>
+__global__ __launch_bounds__(C::NT) void wgrad3x3_group_kernel(WgradGroupArgs g) {
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = group_member(g, g.start, b);
+    wgrad_body<C>(g.d[t], g.ws[t], g.splits, g.tiles, b - g.start[t]);
 }
 
 // dW[co][ci][tap] (reference OIHW) = scale * sum_s ws[s][tap][co'][ci];  co' = kernel channel order.
@@ -334,20 +366,19 @@ __global__ __launch_bounds__(128) void wgrad_reduce_t_kernel(WgradArgs a) {
 // summed through LDS in slice order.  Production <16, 16, 4>; the tuning build picks others
 // with ISR_WGRAD_RED (timing A/B of the cfg3 step).
 template <int RED_SL, int RED_COLS, int UNR>
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
+__device__ __forceinline__ void wgrad_reduce_body(const isr_wgrad_desc& d, const float* ws, int splits, int blk) {
     static_assert(RED_SL * RED_COLS == 256, "one 256-thread block");
     __shared__ f32x4 red[RED_SL][RED_COLS];
-    const isr_wgrad_desc& d = a.d;
     const size_t per = (size_t)9 * d.cout * d.cin;
     const size_t row = per + d.cout;
     const int nv = (int)(row / 4);
     const int lc = threadIdx.x % RED_COLS, slice = threadIdx.x / RED_COLS;
-    const int col = blockIdx.x * RED_COLS + lc;
+    const int col = blk * RED_COLS + lc;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (col < nv) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(a.ws) + col;
+        const f32x4* src = reinterpret_cast<const f32x4*>(ws) + col;
 #pragma unroll UNR
-        for (int sp = slice; sp < a.splits; sp += RED_SL) acc += src[(size_t)sp * (row / 4)];
+        for (int sp = slice; sp < splits; sp += RED_SL) acc += src[(size_t)sp * (row / 4)];
     }
     red[slice][lc] = acc;
     __syncthreads();
@@ -371,6 +402,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
             d.db[co] = acc[e] * d.scale;
         }
     }
+}
+
+template <int RED_SL, int RED_COLS, int UNR>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(WgradArgs a) {
+    wgrad_reduce_body<RED_SL, RED_COLS, UNR>(a.d, a.ws, a.splits, blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_group_kernel(WgradGroupArgs g) {
+    const int b = blockIdx.x;
+    const int t = group_member(g, g.rstart, b);
+    wgrad_reduce_body<16, 16, 4>(g.d[t], g.ws[t], g.splits, b - g.rstart[t]);
 }
 
 template <int SL, int COLS, int UNR>
@@ -562,6 +604,83 @@ size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d, int variant) {
 
 int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s, int parts) {
     return wgrad_pick(d, variant, [&](auto c) { return launch_wgrad<decltype(c)>(d, ws, ws_bytes, s, parts); });
+}
+
+// ---- grouped weight gradients (isr_wgrad3x3_group) ----
+// every member: plain 3x3 (no sub2 / tap window), cout % 32 == cin % 32 == 0, the same n / ha /
+// wa; 32x32 (co, ci) tiles, 8-row stages with 2 waves per kernel row (4-row stages when ha % 8)
+template <class C>
+static int group_plan(const isr_wgrad_desc* ds, int n, WgradGroupArgs* g, size_t* bytes) {
+    if (n < 1 || n > WG_GROUP_MAX) return -2;
+    int pairs = 0;
+    for (int t = 0; t < n; ++t) {
+        const isr_wgrad_desc& d = ds[t];
+        if (d.g_sub2 || d.x_sub2 || d.taps || d.cout % C::CO_T || d.cin % C::CI_T || d.ha % C::TY || d.n != ds[0].n ||
+            d.ha != ds[0].ha || d.wa != ds[0].wa)
+            return -2;
+        pairs += (d.cout / C::CO_T) * (d.cin / C::CI_T);
+    }
+    const int tiles = ds[0].n * (ds[0].ha / C::TY) * (ds[0].wa / 32);
+    int splits = (512 + pairs - 1) / pairs;  // ~512 blocks (the KW == 2 single-conv target)
+#ifdef ISR_TUNING
+    if (const char* e = getenv("ISR_WGRAD_GROUP_SPLITS")) splits = atoi(e);  // split sweep (tuning builds)
+#endif
+    if (splits < 1) splits = 1;
+    if (splits > tiles) splits = tiles;
+    size_t off = 0;
+    int blk = 0, rblk = 0;
+    for (int t = 0; t < n; ++t) {
+        const isr_wgrad_desc& d = ds[t];
+        g->d[t] = d;
+        g->ws[t] = (float*)(uintptr_t)off;  // byte offset for now; based on the workspace below
+        off += ((size_t)splits * 9 * d.cout * d.cin + (size_t)splits * d.cout) * 4;
+        off = (off + 255) / 256 * 256;
+        g->start[t] = blk;
+        blk += splits * (d.cout / C::CO_T) * (d.cin / C::CI_T);
+        g->rstart[t] = rblk;
+        rblk += (int)((((size_t)9 * d.cout * d.cin + d.cout) / 4 + 15) / 16);
+    }
+    g->start[n] = blk;
+    g->rstart[n] = rblk;
+    for (int t = n + 1; t <= WG_GROUP_MAX; ++t) g->start[t] = g->rstart[t] = 0x7fffffff;
+    g->n = n;
+    g->splits = splits;
+    g->tiles = tiles;
+    *bytes = off;
+    return 0;
+}
+
+template <class F>
+static auto group_pick(const isr_wgrad_desc* ds, int n, F&& f) {
+    bool ty8 = true;
+    for (int t = 0; t < n; ++t) ty8 = ty8 && ds[t].ha % 8 == 0;
+    return ty8 ? f(Fam<8, 2>::C11()) : f(Fam<4>::C11());
+}
+
+size_t wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* ds, int n) {
+    return group_pick(ds, n, [&](auto c) -> size_t {
+        WgradGroupArgs g;
+        size_t bytes = 0;
+        return group_plan<decltype(c)>(ds, n, &g, &bytes) == 0 ? bytes : 0;
+    });
+}
+
+int wgrad3x3_group_dispatch(const isr_wgrad_desc* ds, int n, void* ws, size_t ws_bytes, hipStream_t s) {
+    return group_pick(ds, n, [&](auto c) -> int {
+        using C = decltype(c);
+        WgradGroupArgs g;
+        size_t bytes = 0;
+        const int rc = group_plan<C>(ds, n, &g, &bytes);
+        if (rc) return rc;
+        if (ws_bytes < bytes) return -3;
+        for (int t = 0; t < n; ++t) g.ws[t] = (float*)((char*)ws + (uintptr_t)g.ws[t]);
+        auto kern = wgrad3x3_group_kernel<C>;
+        lds_limit((const void*)kern, C::LDS);
+        hipLaunchKernelGGL(kern, dim3(g.start[n]), dim3(C::NT), C::LDS, s, g);
+        if (hipGetLastError() != hipSuccess) return -1;
+        hipLaunchKernelGGL(wgrad_reduce_group_kernel, dim3(g.rstart[n]), dim3(256), 0, s, g);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    });
 }
 
 }  // namespace isr

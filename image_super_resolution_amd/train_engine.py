@@ -37,7 +37,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
-from . import ops
+from . import _lib, ops
 from ._lib import load as _load_lib
 from .ops import ActBuffer
 
@@ -402,6 +402,8 @@ class GeneratorTrainPlan:
         d9h = ops.wgrad9x9_desc(self.dummy_x, self.gf0, _meta_dw(64, 3, 9, dev), None, head=True)
         B.append(("wg9", d9h, ci[id(self.head)]))
         B.append(("ready", "head", False))
+        if _os.environ.get("ISR_TRAIN_WG_GROUP", "1") == "1":
+            B = _group_side_wgrads(B, lib)
         self.bwd_launches = B
         self.head_wg = d9h
         # workspace for the split-K partial sums
@@ -409,6 +411,8 @@ class GeneratorTrainPlan:
         for e in B:
             if e[0] == "wg3":
                 nbytes = max(nbytes, lib.isr_wgrad3x3_workspace_bytes(ctypes.byref(e[1])))
+            elif e[0] == "wg3g":
+                nbytes = max(nbytes, lib.isr_wgrad3x3_group_workspace_bytes(e[1], len(e[2])))
             elif e[0] == "wg9":
                 nbytes = max(nbytes, lib.isr_wgrad9x9_workspace_bytes(ctypes.byref(e[1])))
         if nbytes == 0:
@@ -561,6 +565,15 @@ class GeneratorTrainPlan:
                     rc = lib.isr_wgrad3x3(byref(d), self.ws_side.data_ptr(), self.ws_side.numel(), sst)
                 else:
                     rc = (lib.isr_wgrad3x3 if kind == "wg3" else lib.isr_wgrad9x9)(byref(d), ws, wsn, st)
+            elif kind == "wg3g":  # one RDB's weight gradients in one launch (isr_wgrad3x3_group)
+                for k, c in enumerate(e[2]):
+                    wo, bo = self._conv_goff[c][:2]
+                    d[k].dw = gbase + 4 * wo
+                    d[k].db = gbase + 4 * bo if bo is not None else None
+                if self.side is not None:
+                    rc = lib.isr_wgrad3x3_group(d, len(e[2]), self.ws_side.data_ptr(), self.ws_side.numel(), sst)
+                else:
+                    rc = lib.isr_wgrad3x3_group(d, len(e[2]), ws, wsn, st)
             elif kind == "head":
                 rc = lib.isr_head9x9_fwd(byref(d), st)
             else:
@@ -581,6 +594,36 @@ class GeneratorTrainPlan:
 
 # workspaces in the ring of the side stream's split-K partials (train plan with a reduce stream)
 RED_RING = 4
+
+
+def _group_side_wgrads(B: list, lib) -> list:
+    """Runs of consecutive side-stream 3x3 weight gradients (one RDB's five convs: one dense
+    buffer, one gradient buffer) become ONE ("wg3g", descriptor array, conv indices, True) entry
+    launched through isr_wgrad3x3_group — one grid over all their (co, ci) tile pairs, ~5x fewer
+    split-K partials.  A run the library refuses to group stays as separate launches."""
+    out, run = [], []
+
+    def flush():
+        if len(run) >= 2:
+            arr = (_lib.IsrWgradDesc * len(run))(*[r[1] for r in run])
+            if lib.isr_wgrad3x3_group_workspace_bytes(arr, len(run)) > 0:
+                out.append(("wg3g", arr, [r[2] for r in run], True))
+                run.clear()
+                return
+        out.extend(run)
+        run.clear()
+
+    for e in B:
+        if e[0] == "wg3" and e[3] and len(run) < 5:
+            run.append(e)
+            continue
+        flush()
+        if e[0] == "wg3" and e[3]:
+            run.append(e)
+        else:
+            out.append(e)
+    flush()
+    return out
 
 
 # DDP-style gradient buckets: consecutive backward segments are merged until a bucket holds at

@@ -182,6 +182,14 @@ int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_
  * into dw / db (same descriptor and workspace; the caller orders the second after the first, on
  * another stream too, and keeps the workspace untouched in between).  Lets a caller take the
  * reductions off the stream that chains the weight-gradient kernels (train_engine.py). */
+/* Up to 5 weight gradients over one pixel grid in one launch (plus one reduce launch): the 5 convs
+ * of an RDB (utils/models.py:265-271) read one dense buffer and one gradient buffer; their (co, ci)
+ * tile pairs share one grid, so ~5x fewer split-K partials fill the chip.  Members: plain 3x3
+ * (g_sub2 = x_sub2 = taps = 0), cin / cout multiples of 32, the same n / ha / wa; `splits` is
+ * ignored.  Each member's dw / db / scale as in isr_wgrad3x3; one workspace of
+ * isr_wgrad3x3_group_workspace_bytes(descs, n) bytes. */
+size_t isr_wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* descs, int32_t n);
+int isr_wgrad3x3_group(const isr_wgrad_desc* descs, int32_t n, void* workspace, size_t ws_bytes, isr_stream_t s);
 int isr_wgrad3x3_partials(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
 int isr_wgrad3x3_reduce(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
 /* Tuning: the same computation by an explicit kernel variant (0 = production;
