@@ -621,7 +621,9 @@ static int group_plan(const isr_wgrad_desc* ds, int n, WgradGroupArgs* g, size_t
         pairs += (d.cout / C::CO_T) * (d.cin / C::CI_T);
     }
     const int tiles = ds[0].n * (ds[0].ha / C::TY) * (ds[0].wa / 32);
-    int splits = (512 + pairs - 1) / pairs;  // ~512 blocks (the KW == 2 single-conv target)
+    // ~1024 blocks: the cfg3 step is flat from 28 to 56 splits over an RDB's 26 tile pairs and
+    // loses 0.4 ms at 20, 1.7 ms at 8 (tuning sweep, profiles/r04_wgrad_group_splits.jsonl)
+    int splits = (1024 + pairs - 1) / pairs;
 #ifdef ISR_TUNING
     if (const char* e = getenv("ISR_WGRAD_GROUP_SPLITS")) splits = atoi(e);  // split sweep (tuning builds)
 #endif

@@ -402,8 +402,9 @@ class GeneratorTrainPlan:
         d9h = ops.wgrad9x9_desc(self.dummy_x, self.gf0, _meta_dw(64, 3, 9, dev), None, head=True)
         B.append(("wg9", d9h, ci[id(self.head)]))
         B.append(("ready", "head", False))
-        if _os.environ.get("ISR_TRAIN_WG_GROUP", "1") == "1":
-            B = _group_side_wgrads(B, lib)
+        wg_group = _os.environ.get("ISR_TRAIN_WG_GROUP", "1")
+        if wg_group in ("1", "4"):  # "4": the RDB final conv stays on its own ci-split launch (A/B)
+            B = _group_side_wgrads(B, lib, skip_final=wg_group == "4")
         self.bwd_launches = B
         self.head_wg = d9h
         # workspace for the split-K partial sums
@@ -596,7 +597,7 @@ class GeneratorTrainPlan:
 RED_RING = 4
 
 
-def _group_side_wgrads(B: list, lib) -> list:
+def _group_side_wgrads(B: list, lib, skip_final: bool = False) -> list:
     """Runs of consecutive side-stream 3x3 weight gradients (one RDB's five convs: one dense
     buffer, one gradient buffer) become ONE ("wg3g", descriptor array, conv indices, True) entry
     launched through isr_wgrad3x3_group — one grid over all their (co, ci) tile pairs, ~5x fewer
@@ -613,12 +614,15 @@ def _group_side_wgrads(B: list, lib) -> list:
         out.extend(run)
         run.clear()
 
+    def groupable(e):
+        return e[0] == "wg3" and e[3] and not (skip_final and e[1].cout == 64 and e[1].cin == 192)
+
     for e in B:
-        if e[0] == "wg3" and e[3] and len(run) < 5:
+        if groupable(e) and len(run) < 5:
             run.append(e)
             continue
         flush()
-        if e[0] == "wg3" and e[3]:
+        if groupable(e):
             run.append(e)
         else:
             out.append(e)
