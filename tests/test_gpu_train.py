@@ -142,3 +142,32 @@ def test_resnet_train_step_all_grads_vs_oracle():
     for name, b in m.named_buffers():
         if "running" in name:
             torch.testing.assert_close(b.cpu(), sd[name], rtol=1e-2, atol=1e-3)
+
+
+@pytest.mark.parametrize("env,bitwise", [({"ISR_TRAIN_RED_STREAM": "1"}, True), ({"ISR_TRAIN_WG_GROUP": "0"}, False)])
+def test_backward_options_same_gradients(monkeypatch, env, bitwise):
+    """The A/B options of the backward plan give the production gradients: the side stream's
+    reductions on a third stream (same partials, same sums: bit for bit) and the RDB weight
+    gradients as separate launches instead of one grouped launch (other split-K partition)."""
+    torch.manual_seed(0)
+    sd = synth_state_dict(models.EResNet(2, 0.2, 2).state_dict(), 13)
+    lr, hr01 = synth_lr_batch(2, 32, 32, seed=17, scale=2)
+    x, hr = normalize(lr).to(DEV), (hr01 * 2 - 1).to(DEV)
+
+    def grads():
+        m = models.EResNet(2, 0.2, 2)
+        m.load_state_dict(sd)
+        m = m.to(DEV).train()
+        F.l1_loss(m(x), hr).backward()
+        torch.cuda.synchronize()
+        return {k: p.grad.clone() for k, p in m.named_parameters()}
+
+    ref = grads()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    got = grads()
+    for k in ref:
+        if bitwise:
+            assert torch.equal(got[k], ref[k]), k
+        else:
+            torch.testing.assert_close(got[k], ref[k], rtol=1e-4, atol=1e-5 * ref[k].abs().max().item())
