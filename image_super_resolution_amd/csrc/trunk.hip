@@ -334,9 +334,17 @@ __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src&
 // -DISR_TRUNK_INTERLEAVE=2, of step 2): OFF.  Bit-identical (tests/test_gpu_chain.py) but slower:
 // 7.41 / 7.47 ms per bench forward against 6.64 ms for the block issue, same box, two rounds each
 // (profiles/r03_trunk_interleave_ab.jsonl) — the LDS-DMA issue stalls the wave's in-order MFMA
-// stream wherever it sits, so spreading it only adds the stalls to the matrix-pipe chain.  (A
-// first version also rewrote the refill loop; that rewrite broke the 8-wave form and faulted the
-// card once — the loop is back to its tested form.)
+// stream wherever it sits, so spreading it only adds the stalls to the matrix-pipe chain.  This
+// build (python -m image_super_resolution_amd._build --interleave) passes tests/test_gpu_chain.py
+// bit for bit (round 4).  Round 3's first version also deferred EVERY staged item by one loop
+// pass and re-derived the deferred item's chunk and slot as (so - h0) / pstride and
+// (dst - smem) / SLOT; that run gave wrong 8-wave outputs and faulted the card once.  Both
+// re-derivations are exact (so = h0 + chunk * pstride with the tile offset below one plane, dst =
+// smem + slot * SLOT), the pieces stay inside a slot in both forms and push_mark's positions
+// follow the issue order, so no chunk, slot or offset of that diff can be shown out of range
+// from the code; the run was not repeated.  The bug class is closed instead: every buffer
+// resource carries its tensor's real extent (rsrc_n: an offset past it reads zeros / drops the
+// store), and the tuning build checks chunk < nch, slot < NST and the bias slot before issuing.
 // Wave priority: 1 (production) raises the wave to priority 1 around each chunk's MFMA stream
 // (s_setprio, cdna_hip_programming.md T5), so the co-resident workgroup's refill / epilogue issue
 // yields to it: 6.567 / 6.566 vs 6.620 / 6.592 ms per bench forward, same box, two rounds
