@@ -191,9 +191,11 @@ __device__ __forceinline__ void glds4(const void* gsrc, void* lds) {
 // K-chunks in flight).  <4, 4, 2>: two 4-wave workgroups per CU, one chunk in flight (the
 // round-3 first form); <8, 2, 4>: one 8-wave workgroup per CU, three chunks in flight, two tiles
 // of independent images interleaved per layer.
-template <int WM_, int R_, int NST_, int TH_ = 16, int XM_ = 0>
+template <int WM_, int R_, int NST_, int TH_ = 16, int XM_ = 0, int NTP_ = 0>
 struct TK {
     static constexpr int WM = WM_, R = R_, NST = NST_;
+    // NTP (A/B): non-temporal cache policy on the halo LDS-DMA (bit 0) / the output stores (bit 1)
+    static constexpr int HALO_AUX = 16 | ((NTP_ & 1) ? 2 : 0), STORE_AUX = 16 | ((NTP_ & 2) ? 2 : 0);
     // XM = 1: XCD-aware tile deal — workgroup b (dispatched round-robin to XCD b % 8) works as
     // virtual workgroup xcd_remap(b), so each XCD streams a contiguous range of tiles and a tile's
     // halo neighbours were written through the same XCD's L2
@@ -260,7 +262,7 @@ __device__ __forceinline__ Src src_of(const C& c, const_rec& rec, int t) {
 // weight pieces; wave 0 also the bias (first chunk of a tile).  Halo pieces are sc1 (L1
 // bypass: other workgroups of this launch wrote them).  Returns the vector-memory instructions
 // this wave issued (wave-uniform), for the counted waits.
-template <int WM, int HPW, int WPW, int SLOTB, int BIASB, int HP>
+template <int WM, int HPW, int WPW, int SLOTB, int BIASB, int HP, int HAUX = 16>
 __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t pstride, int abl, const Src& s,
                                                   int chunk, int slot, bool with_bias, int bslot) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -274,7 +276,7 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
         for (int k = 0; k < HPW; ++k) {
             const int j = wave + WM * k;
             if (j < HP) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, ISR_LDS_PTR(dst + j * 1024), 16, hoff[k], so, 0, 16);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, ISR_LDS_PTR(dst + j * 1024), 16, hoff[k], so, 0, HAUX);
                 ++n;
             }
         }
@@ -323,10 +325,10 @@ __device__ __forceinline__ uint32_t stage_chunk(const TrunkCtx<K>& c, const Src&
         uint32_t ho[K::HPW];
 #pragma unroll
         for (int k = 0; k < K::HPW; ++k) ho[k] = halo_piece_off<K::HQ>(wave_id() + K::WM * k, ln, c.wp);
-        return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF, K::HP>(ho, c.pstride, c.abl, s, chunk, slot,
+        return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF, K::HP, K::HALO_AUX>(ho, c.pstride, c.abl, s, chunk, slot,
                                                                           with_bias, bslot);
     }
-    return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF, K::HP>(c.hoff, c.pstride, c.abl, s, chunk, slot,
+    return stage_chunk_k<K::WM, K::HPW, K::WPW, K::SLOT, K::BIAS_OFF, K::HP, K::HALO_AUX>(c.hoff, c.pstride, c.abl, s, chunk, slot,
                                                                       with_bias, bslot);
 }
 
@@ -836,7 +838,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
 #pragma unroll
                     for (int e = 0; e < 8; ++e) tq[e] = (__bf16)u[e];
                     if (!(c.abl & 4)) {
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tq), yr, off, 0, 16);
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tq), yr, off, 0, K::STORE_AUX);
                         ++st.issued;
                     }
                 }
@@ -990,6 +992,8 @@ using TK_T32 = TK<8, 4, 2, 32>;
 // per SIMD at 128 VGPRs (one fragment set), and each wave issues half the refill pieces
 using TK_QUAD = TK<8, 2, 2>;
 using TK_PAIR_X = TK<4, 4, 2, 16, 1>;  // the pair form with the XCD-aware tile deal
+using TK_PAIR_NTH = TK<4, 4, 2, 16, 0, 1>;  // non-temporal halo loads
+using TK_PAIR_NTS = TK<4, 4, 2, 16, 0, 2>;  // non-temporal output stores
 
 int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_deep.hip
 int trunk_deep_knobs_set(const int* k);
@@ -999,6 +1003,8 @@ int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
     if (form == 2) return trunk_launch_k<TK_T32>(cd, s);
     if (form == 4) return trunk_launch_k<TK_QUAD>(cd, s);
     if (form == 5) return trunk_launch_k<TK_PAIR_X>(cd, s);
+    if (form == 6) return trunk_launch_k<TK_PAIR_NTH>(cd, s);
+    if (form == 7) return trunk_launch_k<TK_PAIR_NTS>(cd, s);
     return form == 1 ? trunk_launch_k<TK_DEEP>(cd, s) : trunk_launch_k<TK_PAIR>(cd, s);
 }
 

@@ -404,7 +404,8 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
  * spread over the MFMA stream, neighbourhood polls by LDS-DMA (needs ha % 32 == 0); 5 = trunk.hip's
  * pair tile and ring with two 8-wave workgroups per CU (2 rows per wave, 4 waves per SIMD at
  * 128 VGPRs: one fragment set read a kernel row ahead, half the refill pieces per wave); 6 = the
- * production form with an XCD-aware tile deal (each XCD streams a contiguous range of tiles). */
+ * production form with an XCD-aware tile deal (each XCD streams a contiguous range of tiles); 7 / 8 =
+ * the production form with non-temporal halo loads / output stores. */
 int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
 /* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
  * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,

@@ -64,7 +64,7 @@ def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks):
     xs = _inputs(n, h, w, 3, seed=3)
     refs = _run(gw, xs, chain=False)
     # variants 3 and 4 (32x32 tiles) need the 16-row-rounded height to be a multiple of 32
-    for variant in (0, 6, 5, 2, 1) + ((3, 4) if -(-h // 16) % 2 == 0 else ()):
+    for variant in (0, 7, 8, 6, 5, 2, 1) + ((3, 4) if -(-h // 16) % 2 == 0 else ()):
         for acquire in (False, True):
             for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire, variant=variant), refs):
                 assert torch.equal(out, ref), \
