@@ -654,8 +654,21 @@ static int group_plan(const isr_wgrad_desc* ds, int n, WgradGroupArgs* g, size_t
 
 template <class F>
 static auto group_pick(const isr_wgrad_desc* ds, int n, F&& f) {
-    bool ty8 = true;
-    for (int t = 0; t < n; ++t) ty8 = ty8 && ds[t].ha % 8 == 0;
+    bool ty8 = true, ty16 = true;
+    for (int t = 0; t < n; ++t) {
+        ty8 = ty8 && ds[t].ha % 8 == 0;
+        ty16 = ty16 && ds[t].ha % 16 == 0;
+    }
+#ifdef ISR_TUNING
+    // tile-config probe of the grouped launch (tuning builds): 1 = 4-row stages, 1 wave per row;
+    // 2 = 8-row stages, 4 waves per row; 3 = 16-row stages, 2 waves per row; 4 = 8-row, 1 wave
+    static const int cfg = getenv("ISR_WGRAD_GROUP_CFG") ? atoi(getenv("ISR_WGRAD_GROUP_CFG")) : 0;
+    if (cfg == 1) return f(Fam<4>::C11());
+    if (cfg == 2 && ty8) return f(Fam<8, 4>::C11());
+    if (cfg == 3 && ty16) return f(Fam<16, 2>::C11());
+    if (cfg == 4 && ty8) return f(Fam<8>::C11());
+#endif
+    (void)ty16;
     return ty8 ? f(Fam<8, 2>::C11()) : f(Fam<4>::C11());
 }
 
