@@ -55,11 +55,17 @@ __global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* l
                    v.pad >= 1;
         };
         const int kind = kinds[L];
+        // kind 2 (the training backward's RDB gather convs): a 32-cout layer whose epilogue is the
+        // LeakyReLU' mask of a forward activation instead of a LeakyReLU: v = acc * (m > 0 ? 1 :
+        // mslope), m = channels [m.coff, +32) of a buffer of the same geometry (no r1 / r2)
+        const bool masked = kind == 2;
         if (d.n != n || d.ha != ha || d.wa != wa || d.h != g0.h || d.w != g0.w) e |= 1;
-        if (!same_geo(d.x) || !same_geo(d.y) || (d.r2.data && !same_geo(d.r2))) e |= 2;
-        if (kind == 0 ? d.cout != 32 : (kind == 1 ? d.cout != 64 : true)) e |= 4;
+        if (!same_geo(d.x) || !same_geo(d.y) || (d.r2.data && !same_geo(d.r2)) || (masked && !same_geo(d.m))) e |= 2;
+        if (kind == 0 || kind == 2 ? d.cout != 32 : (kind == 1 ? d.cout != 64 : true)) e |= 4;
         if (d.cin % 16 || d.cin < 64 || d.cin / 16 > 120 || !d.bias || ((uintptr_t)d.bias & 15)) e |= 8;
-        if (d.shuffle != 1 || d.x_sub2 || d.taps || d.m.data || d.y2.data) e |= 16;
+        if (d.shuffle != 1 || d.x_sub2 || d.taps || d.y2.data || (d.m.data != nullptr) != masked ||
+            (masked && (d.m_c0 != 0 || d.slope != 1.f || d.r1.data || d.r2.data || d.s1 != 1.f || d.s2 != 1.f)))
+            e |= 16;
         int fold = 0;
         uint16_t idv = 0;
         if (d.r1.data) {
@@ -92,11 +98,12 @@ __global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* l
         rec.y = (uint64_t)(uintptr_t)d.y.data;
         rec.w = (uint64_t)(uintptr_t)d.wpack;
         rec.b = (uint64_t)(uintptr_t)d.bias;
-        rec.r2 = (uint64_t)(uintptr_t)d.r2.data;
+        rec.r2 = (uint64_t)(uintptr_t)(masked ? d.m.data : d.r2.data);  // kind 2: the mask buffer
         rec.planes = (uint32_t)(d.x.coff / 16) | (uint32_t)(d.y.coff / 16) << 16;
-        rec.shape = (uint32_t)(d.r2.coff / 16) | (uint32_t)(d.cin / 16) << 16 | (uint32_t)(kind & 255) << 24;
+        rec.shape = (uint32_t)((masked ? d.m.coff : d.r2.coff) / 16) | (uint32_t)(d.cin / 16) << 16 |
+                    (uint32_t)(kind & 255) << 24;
         rec.deps = (uint32_t)first_new | (uint32_t)fold << 8 | (uint32_t)idv << 16;
-        rec.slope = d.slope;
+        rec.slope = masked ? d.mslope : d.slope;
         rec.s1 = d.s1;
         rec.s2 = d.s2;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&rec);
@@ -252,7 +259,7 @@ __device__ __forceinline__ Src src_of(const C& c, const_rec& rec, int t) {
                        (bx * tk::TW - 1 + c.pad)) * 32);
     s.w = (const char*)(uintptr_t)rec.w;
     s.b = (const float*)(uintptr_t)rec.b;
-    s.wpc = rec_kind(rec) == 0 ? tk::WPG : tk::WPF;
+    s.wpc = rec_kind(rec) == 1 ? tk::WPF : tk::WPG;  // 64 / 32 couts (kinds 0 and 2: 32)
     s.xbytes = c.abytes;
     s.wbytes = (uint32_t)(rec_nch(rec) * s.wpc * 1024);
     return s;
@@ -516,6 +523,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     const unsigned need = c.gen * 1024u + (unsigned)L;  // the neighbourhood is done with layer L-1
     const bool fold = NF == 2 && rec_fold(rec);
     const bool has_r2 = NF == 2 && rec.r2 != 0;
+    const bool masked = NF == 1 && rec_kind(rec) == 2;  // gather conv: LeakyReLU' mask from rec.r2
     const Src me = src_of(c, rec, t);
     bool dep_ok = first_new == tk::NEED_NONE || st.dep_next;
     st.dep_next = false;
@@ -801,10 +809,10 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                 }
             st.issued += NF * 2;
         };
-        if (has_r2) load_r2(0);
+        if (has_r2 || masked) load_r2(0);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (has_r2 && r + 1 < R) load_r2(r + 1);
+            if ((has_r2 || masked) && r + 1 < R) load_r2(r + 1);
             const int yy = y0 + wave * R + r;
             const bool valid = yy < c.h && xx < c.w;
             const uint32_t pix = (uint32_t)((yy + c.pad) * c.wp + xx + c.pad);
@@ -823,7 +831,10 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                     float* u = v + 8 * blk;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
-                        u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
+                        if (masked)
+                            u[e] = (float)q2[r][f][blk][e] > 0.f ? u[e] : u[e] * slope;
+                        else
+                            u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
                         if (fold) u[e] = u[e] * s1;
                         if (has_r2) {
                             u[e] = u[e] * s2 + (float)q2[r][f][blk][e];
@@ -927,7 +938,7 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
                     const int bx2 = nx.t % c.nbx, nq = nx.t / c.nbx, by2 = nq % c.nby, im2 = nq / c.nby;
                     nx.self_dep = im == im2 && abs(bx - bx2) <= 1 && abs(by - by2) <= 1;
                 }
-                if (rec_kind(rec) == 0) run_tile<K, 1>(c, st, rec, L, t, nx);
+                if (rec_kind(rec) != 1) run_tile<K, 1>(c, st, rec, L, t, nx);
                 else run_tile<K, 2>(c, st, rec, L, t, nx);
             }
         }

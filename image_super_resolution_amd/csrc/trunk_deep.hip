@@ -733,7 +733,8 @@ __global__ __launch_bounds__(td::NT, 2) void trunk_deep_kernel(unsigned* state, 
     bool shape_ok = true;
     for (int L = 0; L < nl; ++L) {
         const int n = rec_nch(c.recs[L]);
-        shape_ok = shape_ok && (n % 2 == 0) && n >= 2 && (rec_kind(c.recs[L]) == 0 || (rec_fold(c.recs[L]) && n >= 6));
+        shape_ok = shape_ok && (n % 2 == 0) && n >= 2 && rec_kind(c.recs[L]) != 2 &&
+                   (rec_kind(c.recs[L]) == 0 || (rec_fold(c.recs[L]) && n >= 6));  // no masked (kind 2) layers
     }
     if (!shape_ok) {
         if (threadIdx.x == 0 && blockIdx.x == 0) {

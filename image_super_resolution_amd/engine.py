@@ -257,20 +257,28 @@ class ConvChain:
     """Device-side layer table + state for isr_conv_chain over a run of RDB convs
     (growth convs: kind 0; 192→64 final convs: kind 1) sharing one tile grid."""
 
-    def __init__(self, descs, grid: ActBuffer, device, acquire: bool = False, variant: int | None = None):
+    def __init__(self, descs, grid: ActBuffer, device, acquire: bool = False, variant: int | None = None,
+                 state: torch.Tensor | None = None):
+        """`state`: share another chain's state words (chains launched one after another on one
+        stream: generations and progress words are serial, and one give-up count guards both)."""
         lib = ops._lib.load()
         kinds = []
         g = descs[0].x
         for d in descs:
             ops.check(lib.isr_conv3x3_check(ctypes.byref(d)), "chain layer")
             if d.cout == 32:
-                kinds.append(0)
+                # kind 2: the training backward's RDB gather conv (LeakyReLU' mask epilogue)
+                kinds.append(2 if d.m.data else 0)
             elif d.cin == 192 and d.cout == 64:
                 kinds.append(1)
             else:
                 raise ValueError(f"conv chain: unsupported layer {d.cin}->{d.cout}")
-            if d.x_sub2 or d.taps or d.shuffle != 1 or d.m.data or d.y2.data:
+            if d.x_sub2 or d.taps or d.shuffle != 1 or d.y2.data:
                 raise ValueError("conv chain: plain 3x3 layers only")
+            if d.m.data and (d.m_c0 != 0 or d.slope != 1.0 or d.r1.data or d.r2.data or d.s1 != 1.0 or d.s2 != 1.0
+                             or (d.m.hp, d.m.wp, d.m.cs, d.m.pad) != (g.hp, g.wp, g.cs, g.pad)):
+                raise ValueError("conv chain: a masked layer is a plain 32-cout conv whose every channel is "
+                                 "masked by a buffer of the chain's geometry")
             if (d.n, d.ha, d.wa) != (grid.n, grid.ha, grid.wa):
                 raise ValueError("conv chain: every layer must share the tile grid")
             # the trunk kernel's layer records (trunk.hip) share one view geometry and fold r1
@@ -289,6 +297,8 @@ class ConvChain:
         if self.variant in (3, 4) and grid.ha % 32:
             raise ValueError(f"conv chain: variant {self.variant} (32x32 trunk tiles) needs the padded height "
                              "a multiple of 32")
+        if 2 in kinds and self.variant in (1, 4):
+            raise ValueError(f"conv chain: variant {self.variant} has no masked (kind 2) layers")
         if self.variant == 4 and any(d.cin % 32 or (k == 1 and (not d.r1.data or d.cin < 96))
                                      for d, k in zip(descs, kinds)):
             raise ValueError("conv chain: variant 4 pairs 16-channel chunks (cin % 32 == 0) and needs every "
@@ -297,7 +307,12 @@ class ConvChain:
         self._table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
         self._kinds = torch.tensor(kinds, dtype=torch.int32, device=device)
         words = lib.isr_conv_chain_state_words(grid.n, grid.ha, grid.wa)
-        self.state = torch.zeros(words, dtype=torch.int32, device=device)
+        if state is not None:
+            if state.numel() < words or state.dtype != torch.int32:
+                raise ValueError("conv chain: shared state too small")
+            self.state = state
+        else:
+            self.state = torch.zeros(words, dtype=torch.int32, device=device)
         self.desc = ops._lib.IsrChainDesc(self._table.data_ptr(), self._kinds.data_ptr(), len(descs), grid.n,
                                           grid.ha, grid.wa, self.state.data_ptr(), int(acquire))
         self.nl = len(descs)

@@ -221,14 +221,17 @@ class GeneratorTrainPlan:
             gp = self.gpacks[j]
             for t in list(range(3, -1, -1)) + ["x"]:
                 out = gp[t]
+                # the x target's pack carries 1 / res: its conv adds the RDB output gradient with s1 = 1
+                # (v = (acc / res + g_out) * res), which the persistent backward chain folds exactly
+                sx = 1.0 / res if t == "x" else 1.0
                 if t == "x":
                     n0, co, srcs = 0, 64, list(range(3, -1, -1))
                 else:
                     n0, co, srcs = 64 + 32 * t, 32, list(range(3, t, -1))
-                items.append((c5.w, out, 64, co, True, False, a * res, n0, 192, 0))
+                items.append((c5.w, out, 64, co, True, False, a * res * sx, n0, 192, 0))
                 for k in srcs:
                     off = 64 + 32 * (3 - k)  # input-channel offset of g_k in the gather input
-                    items.append((cs[k].w, out, 32, co, True, False, 1.0, n0, cs[k].cin, (off // 16) * 9 * co * 16))
+                    items.append((cs[k].w, out, 32, co, True, False, sx, n0, cs[k].cin, (off // 16) * 9 * co * 16))
         return items
 
     def _build(self):
@@ -334,7 +337,8 @@ class GeneratorTrainPlan:
             # ("evrec" / "evwait"), beside the next RDBs' gather convs.
             nr = len(self.rdbs)
             self.Eg = [ActBuffer.alloc(n_, h_, w_, 192, 1, dev) for n_, h_, w_ in [(D[0].n, D[0].h, D[0].w)] * nr]
-            self.gtrunk = ActBuffer.alloc(D[0].n, D[0].h, D[0].w, 64, 1, dev)
+            # 192 channels (64 used): the persistent backward chain needs one buffer geometry
+            self.gtrunk = ActBuffer.alloc(D[0].n, D[0].h, D[0].w, 192, 1, dev)
             # conv1's input gradient (g_R of the last RRDB) goes straight into E_{nr-1}[0:64]
             B[-1] = ("conv", ops.conv3x3_desc(g1, 64, c.bwd, None, 64, self.Eg[nr - 1]))
             for i in range(nb - 1, -1, -1):
@@ -345,7 +349,7 @@ class GeneratorTrainPlan:
                     for t in range(3, -1, -1):
                         slot = 64 + 32 * (3 - t)
                         B.append(("conv", ops.conv3x3_desc(E, slot, gp[t], None, 32, E, y_coff=slot, m=Dj,
-                                                           m_coff=64 + 32 * t, m_c0=0, mslope=LEAKY)))
+                                                           m_coff=64 + 32 * t, m_c0=0, mslope=LEAKY), "gather"))
                     B.append(("evrec", j))
                     B.append(("evwait", j))
                     wg3(Dj, 192, E, 64, cs[4], scale=a * res, side=True)
@@ -353,14 +357,13 @@ class GeneratorTrainPlan:
                         wg3(Dj, cs[t].cin, E, 32, cs[t], g_coff=64 + 32 * (3 - t), side=True)
                     if step == 2:  # RRDB i's weight gradients are all enqueued (side stream)
                         B.append(("ready", i, True))
-                    # v = (acc / res + g_out) * res (+ g_R: the RRDB's own residual, first RDB)
+                    # v = (acc' + g_out) * res (+ g_R: the RRDB's own residual, first RDB); the pack
+                    # carries 1 / res, so acc' = acc / res
                     kw = dict(r2=self.Eg[3 * i + 2]) if step == 2 else {}
-                    # r1_cn=64 (= every output channel, the same sums) keeps this conv on the plain
-                    # 192->64 kernel: with r1 aliasing x, cout 64 and 1/s1 exact (res = 1) libisr
-                    # would pick the residual-fold form the inference trunk needs for bit-identity,
-                    # which costs the per-conv kernel registers (scratch spills)
-                    B.append(("conv", ops.conv3x3_desc(E, 192, gp["x"], None, 64, gout, r1=E, s1=1.0 / res, s2=res,
-                                                       r1_cn=64, **kw)))
+                    # r1_cn=64 (= every output channel, the same sums) keeps the per-conv launch on the
+                    # plain 192->64 kernel; the persistent backward chain folds r1 (r1_cn = 0)
+                    B.append(("conv", ops.conv3x3_desc(E, 192, gp["x"], None, 64, gout, r1=E, s1=1.0, s2=res,
+                                                       r1_cn=64, **kw), "gather"))
             U = self.gtrunk
         for i in range(nb - 1, -1, -1) if not self.gather else ():
             # g_R (gradient wrt the RRDB output) is in U[0:64]
@@ -402,6 +405,9 @@ class GeneratorTrainPlan:
         d9h = ops.wgrad9x9_desc(self.dummy_x, self.gf0, _meta_dw(64, 3, 9, dev), None, head=True)
         B.append(("wg9", d9h, ci[id(self.head)]))
         B.append(("ready", "head", False))
+        self.bchain = None
+        if self.gather and _os.environ.get("ISR_TRAIN_BWD_CHAIN", "0") == "1" and not _device_shared():
+            B = self._backward_chain(B)
         wg_group = _os.environ.get("ISR_TRAIN_WG_GROUP", "1")
         if wg_group in ("1", "4"):  # "4": the RDB final conv stays on its own ci-split launch (A/B)
             B = _group_side_wgrads(B, lib, skip_final=wg_group == "4")
@@ -464,6 +470,46 @@ class GeneratorTrainPlan:
         for i in range(nr // 3):
             seg[i] = (first(1 + 15 * i), first(1 + 15 * (i + 1)))
         self._segments = seg
+
+    def _backward_chain(self, B: list) -> list:
+        """The RDB gather convs of the backward (240 for 16 RRDBs) as ONE persistent isr_conv_chain
+        launch (trunk.hip: the forward dense block's dependency shape — gather t reads
+        E[0:64 + 32 (3 - t)) and writes the next 32 channels, masked by LeakyReLU' of the forward
+        activation (kind 2); the x gather folds the RDB output gradient, r1 = E[0:64]).  The chain
+        owns the whole chip, so the side stream's weight gradients start after it, and DDP's first
+        bucket is flushed after it too (an all-reduce beside it would take CUs its grid needs).
+        Shares the forward chain's state: one give-up count guards the step's optimiser updates.
+        A/B option (ISR_TRAIN_BWD_CHAIN=1, off): correct (tests/test_gpu_train.py) but 52.87 vs
+        52.23 ms per cfg3 step, same box (profiles/r04_train_bwd_chain_ab.jsonl) — the weight
+        gradients it pushes behind the chain had been overlapping the per-conv gathers."""
+        from .engine import CHAIN_ACQUIRE, ConvChain
+        gathers = [k for k, e in enumerate(B) if e[0] == "conv" and len(e) > 2 and e[2] == "gather"]
+        if not gathers:
+            return B
+        zb = torch.zeros(64, device=self.device)
+        self._bchain_bias = zb
+        descs = []
+        for k in gathers:
+            d = IsrConvDescCopy(B[k][1])
+            d.bias = zb.data_ptr()
+            if d.cout == 64:
+                d.r1_cn = 0  # fold the RDB output gradient (r1 aliases the gather input)
+            descs.append(d)
+        try:
+            self.bchain = ConvChain(descs, self.D[0], self.device, acquire=CHAIN_ACQUIRE, variant=0,
+                                    state=self.chain.state if self.chain is not None else None)
+        except ValueError as err:
+            import warnings
+            warnings.warn(f"training backward gathers run per conv (persistent chain refused: {err})")
+            self.bchain = None
+            return B
+        first, last = gathers[0], gathers[-1]
+        body = [e for e in B[first:last + 1] if not (e[0] == "conv" and len(e) > 2 and e[2] == "gather")
+                and e[0] not in ("evrec", "evwait")]
+        head = [e for e in B[:first] if not (e[0] == "ready" and e[1] == "tail")]
+        tail_ready = [e for e in B[:first] if e[0] == "ready" and e[1] == "tail"]
+        return (head + [("bchain", self.bchain)] + tail_ready + [("evrec", "bchain"), ("evwait", "bchain")]
+                + body + B[last + 1:])
 
     # -------------------------------------------------------------- execution
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -538,6 +584,8 @@ class GeneratorTrainPlan:
                 continue
             if kind == "conv":
                 rc = lib.isr_conv3x3_fwd(byref(d), st)
+            elif kind == "bchain":
+                rc = d.fn(byref(d.desc), st)
             elif kind == "bnb":
                 _, _, go, bo2 = self._conv_goff[e[2]]
                 d.dgamma, d.dbeta = gbase + 4 * go, gbase + 4 * bo2
@@ -591,6 +639,13 @@ class GeneratorTrainPlan:
         for p, off in zip(self._params, self._goff):
             out.append(grads[off:off + p.numel()].view(p.shape))
         return out
+
+
+def IsrConvDescCopy(d):
+    """An independent copy of an isr_conv_desc (ctypes structures assign by value)."""
+    c = type(d)()
+    ctypes.pointer(c)[0] = d
+    return c
 
 
 # workspaces in the ring of the side stream's split-K partials (train plan with a reduce stream)

@@ -144,11 +144,14 @@ def test_resnet_train_step_all_grads_vs_oracle():
             torch.testing.assert_close(b.cpu(), sd[name], rtol=1e-2, atol=1e-3)
 
 
-@pytest.mark.parametrize("env,bitwise", [({"ISR_TRAIN_RED_STREAM": "1"}, True), ({"ISR_TRAIN_WG_GROUP": "0"}, False)])
+@pytest.mark.parametrize("env,bitwise", [({"ISR_TRAIN_RED_STREAM": "1"}, True), ({"ISR_TRAIN_WG_GROUP": "0"}, False),
+                                         ({"ISR_TRAIN_BWD_CHAIN": "1"}, False)])
 def test_backward_options_same_gradients(monkeypatch, env, bitwise):
     """The A/B options of the backward plan give the production gradients: the side stream's
-    reductions on a third stream (same partials, same sums: bit for bit) and the RDB weight
-    gradients as separate launches instead of one grouped launch (other split-K partition)."""
+    reductions on a third stream (same partials, same sums: bit for bit), the RDB weight
+    gradients as separate launches instead of one grouped launch (other split-K partition), and
+    the RDB gather convs on the persistent backward chain instead of per-conv launches (the chain
+    folds the RDB output gradient by MFMA, the per-conv launch adds it in the epilogue)."""
     torch.manual_seed(0)
     sd = synth_state_dict(models.EResNet(2, 0.2, 2).state_dict(), 13)
     lr, hr01 = synth_lr_batch(2, 32, 32, seed=17, scale=2)
@@ -166,8 +169,16 @@ def test_backward_options_same_gradients(monkeypatch, env, bitwise):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     got = grads()
+    if "ISR_TRAIN_BWD_CHAIN" in env:
+        m = models.EResNet(2, 0.2, 2)
+        m.load_state_dict(sd)
+        m = m.to(DEV).train()
+        F.l1_loss(m(x), hr).backward()
+        assert m.__dict__["_isr_train_plan"].bchain is not None  # the option really ran the chain
     for k in ref:
         if bitwise:
             assert torch.equal(got[k], ref[k]), k
-        else:
-            torch.testing.assert_close(got[k], ref[k], rtol=1e-4, atol=1e-5 * ref[k].abs().max().item())
+        else:  # bf16 gradient buffers round differently: compare as the oracle bars do, 10x tighter
+            rel = ((got[k] - ref[k]).norm() / ref[k].norm().clamp_min(1e-12)).item()
+            cos = F.cosine_similarity(got[k].flatten().double(), ref[k].flatten().double(), dim=0).item()
+            assert rel <= 5e-3 and cos >= 0.9999, f"{k}: rel {rel:.3e} cos {cos:.6f}"
