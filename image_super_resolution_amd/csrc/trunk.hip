@@ -510,7 +510,7 @@ __device__ __forceinline__ void force_publish(const TrunkCtx<K>& c, Stream<K>& s
     st.pend_t = -1;
 }
 
-template <class K, int NF>
+template <class K, int NF, bool MASKED = false>
 __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, const_rec& rec, int L, int t,
                                          const Next& nx) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -523,7 +523,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     const unsigned need = c.gen * 1024u + (unsigned)L;  // the neighbourhood is done with layer L-1
     const bool fold = NF == 2 && rec_fold(rec);
     const bool has_r2 = NF == 2 && rec.r2 != 0;
-    const bool masked = NF == 1 && rec_kind(rec) == 2;  // gather conv: LeakyReLU' mask from rec.r2
+    constexpr bool masked = NF == 1 && MASKED;  // kind 2 (gather conv): LeakyReLU' mask from rec.r2
     const Src me = src_of(c, rec, t);
     bool dep_ok = first_new == tk::NEED_NONE || st.dep_next;
     st.dep_next = false;
@@ -938,7 +938,9 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
                     const int bx2 = nx.t % c.nbx, nq = nx.t / c.nbx, by2 = nq % c.nby, im2 = nq / c.nby;
                     nx.self_dep = im == im2 && abs(bx - bx2) <= 1 && abs(by - by2) <= 1;
                 }
-                if (rec_kind(rec) != 1) run_tile<K, 1>(c, st, rec, L, t, nx);
+                const int kind = rec_kind(rec);
+                if (kind == 0) run_tile<K, 1>(c, st, rec, L, t, nx);
+                else if (kind == 2) run_tile<K, 1, true>(c, st, rec, L, t, nx);  // the backward chain's gathers
                 else run_tile<K, 2>(c, st, rec, L, t, nx);
             }
         }
