@@ -40,9 +40,12 @@ __device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int NCO_, int NCI_, int TY_, int KW_ = 1, int TWN_ = 0, int CW_ = 1>
+template <int NCO_, int NCI_, int TY_, int KW_ = 1, int TWN_ = 0, int CW_ = 1, int NSTG_ = 2>
 struct WG {
     static constexpr int NCO = NCO_, NCI = NCI_, TY = TY_;
+    // LDS stages in the pixel-tile ring: 2 (stage t+1 lands while stage t computes) or 3 (two
+    // stages in flight: the weight-gradient loop had waited on its staging, PMC wait_any 0.48)
+    static constexpr int NSTG = NSTG_;
     // CW waves per (kernel row, K-share) split the block's NCI ci tiles between them: the block
     // stages each pixel tile's G and X planes ONCE for all its ci tiles (CW = NCI: every 32-ci
     // tile of the layer in one block, so G is not re-staged per ci tile)
@@ -68,7 +71,7 @@ struct WG {
     static constexpr int G_INSTR = GPL * G_IPL, INSTR = G_INSTR + XPL * X_IPL;
     static constexpr int IPW = (INSTR + WM - 1) / WM;
     static constexpr int RED = CW * (KW - 1) * TN * 64 * (TN * NCO * NCIW * 16 + NCO) * 4;  // cross-wave K reduction
-    static constexpr int LDS = 2 * STAGE > RED ? 2 * STAGE : RED;
+    static constexpr int LDS = NSTG * STAGE > RED ? NSTG * STAGE : RED;
     static_assert(LDS <= 163840, "LDS budget");
     static_assert((2 * TY) % KW == 0, "K groups split evenly between the KW waves of a row");
 };
@@ -78,6 +81,18 @@ struct WgradArgs {
     float* ws;  // [splits][9*cout*cin (tap, co, ci) + cout (bias)]
     int splits, tiles;
 };
+
+// s_waitcnt vmcnt(n) for a run-time n in 0..15 (larger: 15 stays correct only as an upper
+// bound of what may remain, so it waits for everything instead)
+__device__ __forceinline__ void wait_vm_upto15(uint32_t n) {
+#define ISR_W15(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    switch (n) {
+        ISR_W15(1) ISR_W15(2) ISR_W15(3) ISR_W15(4) ISR_W15(5) ISR_W15(6) ISR_W15(7) ISR_W15(8)
+        ISR_W15(9) ISR_W15(10) ISR_W15(11) ISR_W15(12) ISR_W15(13) ISR_W15(14) ISR_W15(15)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef ISR_W15
+}
 
 // One block's work: (ci tile, co tile, split) = the block index b within its conv.
 template <class C>
@@ -177,13 +192,23 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
     const int a_lane = gi * C::G_PLANE + (8 * hh + q) * 32 + 8 * p;
     const int b_lane = C::G_BYTES + gi * C::X_PLANE + (8 * hh + q) * 32 + 8 * p;
 
-    if (t0 < t1) stage(t0, 0);
+    // this wave's copies per stage (wave-uniform)
+    const int nps = (C::INSTR - wave + C::WM - 1) / C::WM < C::IPW ? (C::INSTR - wave + C::WM - 1) / C::WM : C::IPW;
+#pragma unroll
+    for (int s0 = 0; s0 < C::NSTG - 1; ++s0)
+        if (t0 + s0 < t1) stage(t0 + s0, s0);
     for (int t = t0; t < t1; ++t) {
-        const int cur = (t - t0) & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int cur = (t - t0) % C::NSTG;
+        if constexpr (C::NSTG == 2) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            // stage t landed; the younger stages already issued may stay in flight
+            const int younger = t1 - 1 - t < C::NSTG - 2 ? t1 - 1 - t : C::NSTG - 2;
+            wait_vm_upto15((uint32_t)(younger * nps));
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (t + 1 < t1) stage(t + 1, cur ^ 1);
+        if (t + C::NSTG - 1 < t1) stage(t + C::NSTG - 1, (t + C::NSTG - 1 - t0) % C::NSTG);
         const char* base = smem + cur * C::STAGE;
 #pragma unroll
         for (int kk = 0; kk < 2 * TY / C::KW; ++kk) {
@@ -667,6 +692,9 @@ static auto group_pick(const isr_wgrad_desc* ds, int n, F&& f) {
     if (cfg == 2 && ty8) return f(Fam<8, 4>::C11());
     if (cfg == 3 && ty16) return f(Fam<16, 2>::C11());
     if (cfg == 4 && ty8) return f(Fam<8>::C11());
+    if (cfg == 5) return f(WG<1, 1, 4, 1, 0, 1, 3>());          // 4-row stages, 3-stage ring
+    if (cfg == 6) return f(WG<1, 1, 4, 2, 0, 1, 3>());          // 4-row stages, 2 waves per row, 3 stages
+    if (cfg == 7 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 3>());   // production tile, 3 stages (1 block / CU)
 #endif
     (void)ty16;
     return ty8 ? f(Fam<8, 2>::C11()) : f(Fam<4>::C11());
