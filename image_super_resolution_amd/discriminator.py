@@ -317,6 +317,11 @@ class _DiscFn(torch.autograd.Function):
     def backward(ctx, gfeat):
         plan = ctx.lease.plan
         dx, grads = plan.backward(gfeat.contiguous(), ctx.needs_input_grad[0], any(ctx.needs_input_grad[2:]))
+        # the plan's buffers (activations, BN accumulators, gradient buffers) are in use until this
+        # backward's kernels finish on this stream: a call on another stream waits for this event
+        plan.done_event = torch.cuda.Event()
+        plan.done_event.record()
+        plan.done_stream = torch.cuda.current_stream()
         ctx.lease.release()
         return (dx, None, *grads)
 
@@ -341,6 +346,9 @@ def conv_stack_train(dis: nn.Module, x: torch.Tensor) -> torch.Tensor:
             raise RuntimeError("discriminator: more than 8 live forward graphs")
         plan = DiscriminatorPlan(dis, n, h, w, x.device)
         plans.append(plan)
+    ev = getattr(plan, "done_event", None)
+    if ev is not None and getattr(plan, "done_stream", None) != torch.cuda.current_stream():
+        torch.cuda.current_stream().wait_event(ev)  # an earlier backward on another stream used it
     plan.pack()
     with torch.autocast("cuda", enabled=False):
         if not (torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in plan.params()))):

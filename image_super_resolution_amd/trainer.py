@@ -30,6 +30,7 @@ Differences, all deliberate:
 from __future__ import annotations
 
 import contextlib
+import os
 import time
 
 import torch
@@ -115,6 +116,10 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
     total = steps if steps is not None else len(batches)
     it = iter(batches)
     pending = []
+    # the discriminator's forwards + backward on a second stream beside the generator's backward
+    # (same results, tests/test_gpu_train_cfg3.py; A/B: ISR_TRAIN_D_OVERLAP=0)
+    overlap = os.environ.get("ISR_TRAIN_D_OVERLAP", "1") == "1"
+    d_stream = torch.cuda.Stream(device) if overlap and device.type == "cuda" else None
     for idx in range(total):
         hr_images, lr_images = transform(next(it))
         sr_images = gen_net(lr_images)
@@ -129,7 +134,18 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
         perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(sr_images, hr_images,
                                                                                          sr_discriminated)
         optimizer_g.zero_grad(set_to_none=True)
+        if d_stream is not None:
+            fwd_done = torch.cuda.Event()
+            fwd_done.record()  # sr / hr and every forward the D step reads
         gradscaler_gen.scale(perceptual_loss).backward()
+        if d_stream is not None:
+            # the discriminator's forwards and backward on a second stream, beside the generator's
+            # backward (they read neither its gradients nor anything it writes; D's weights change
+            # only in D's optimiser step, after both)
+            d_stream.wait_event(fwd_done)
+            with torch.cuda.stream(d_stream):
+                adversarial_loss = _d_forward_backward(dis_net, compute_loss, sr_images, hr_images, optimizer_d,
+                                                       gradscaler_dis)
         gradscaler_gen.unscale_(optimizer_g)
         clip_grad_norm_(gen_net.parameters(), 10)
         guard = step_guard_ptr(_unwrap(gen_net))  # a failed trunk forward updates neither G nor D
@@ -139,12 +155,11 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
             schedule_g.step()
             ema.update(_unwrap(gen_net))
 
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            sr_discriminated = dis_net(sr_images.detach())
-            hr_discriminated = dis_net(hr_images)
-        adversarial_loss = compute_loss.calc_advLoss(sr_discriminated, hr_discriminated)
-        optimizer_d.zero_grad(set_to_none=True)
-        gradscaler_dis.scale(adversarial_loss).backward()
+        if d_stream is not None:
+            torch.cuda.current_stream().wait_stream(d_stream)
+        else:
+            adversarial_loss = _d_forward_backward(dis_net, compute_loss, sr_images, hr_images, optimizer_d,
+                                                   gradscaler_dis)
         if dist_group is not None:
             allreduce_grads(dis_net.parameters(), None if dist_group is True else dist_group)
         gradscaler_dis.unscale_(optimizer_d)
@@ -165,6 +180,17 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
             pending = []
     _verify(gen_net)
     return loss_g
+
+
+def _d_forward_backward(dis_net, compute_loss, sr_images, hr_images, optimizer_d, gradscaler_dis):
+    """train.py:114-119 up to the discriminator's backward (its step follows in the caller)."""
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        sr_discriminated = dis_net(sr_images.detach())
+        hr_discriminated = dis_net(hr_images)
+    adversarial_loss = compute_loss.calc_advLoss(sr_discriminated, hr_discriminated)
+    optimizer_d.zero_grad(set_to_none=True)
+    gradscaler_dis.scale(adversarial_loss).backward()
+    return adversarial_loss
 
 
 class StepTimer:

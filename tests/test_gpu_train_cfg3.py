@@ -120,3 +120,39 @@ def test_cfg3_two_sample_slice_vs_oracle():
         assert rel <= 5e-2 and cos >= 0.998, f"{name}: rel {rel:.3e} cos {cos:.5f}"
     worst.sort(reverse=True)
     print("cfg3 2-sample slice, worst grads vs oracle:", worst[:3])
+
+
+def test_srgan_d_overlap_same_updates(monkeypatch):
+    """train_srgan with the discriminator's forwards + backward on a second stream beside the
+    generator's backward (default) updates G and D exactly as the serial order (bit for bit)."""
+    def run(overlap):
+        monkeypatch.setenv("ISR_TRAIN_D_OVERLAP", "1" if overlap else "0")
+        torch.manual_seed(0)
+        gen = models.SRGAN(2, 0.2, True, SCALE)
+        gen.load_state_dict(synth_state_dict(gen.state_dict(), 9))
+        gen = gen.to(DEV)
+        dis = models.Discriminator(3, 64, 8, 1024).to(DEV)
+        dis.use_libisr(True)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            gl = L.gen_loss(device=DEV, beforeAct=True)
+        mean, std = list(data.IMAGENET_MEAN), list(data.IMAGENET_STD)
+        og = optim.FusedAdam(gen.parameters(), lr=1e-4)
+        od = optim.FusedAdam(dis.parameters(), lr=1e-4)
+        sg = torch.optim.lr_scheduler.LinearLR(og, 1, 0.01, total_iters=2)
+        sd = torch.optim.lr_scheduler.LinearLR(od, 1, 0.01, total_iters=2)
+        ema = models.ModelEMA(gen, tau=2)
+        ema.ema.to(DEV)
+        sc = (torch.amp.GradScaler("cuda", enabled=False), torch.amp.GradScaler("cuda", enabled=False))
+        tf = data.GPUTransform(SCALE, hr_norm=True, mean=mean, std=std, device=DEV)
+        batches = data.SyntheticSR(4, 128, seed=5, device=DEV)
+        losses = trainer.train_srgan(gen, ema, dis, batches, tf, gl, og, od, sc, (sg, sd), 0, None, mean=mean,
+                                     std=std, steps=2, log_every=1)
+        torch.cuda.synchronize()
+        return losses, [p.detach().clone() for p in gen.parameters()], [p.detach().clone() for p in dis.parameters()]
+
+    l0, g0, d0 = run(False)
+    l1, g1, d1 = run(True)
+    assert l0 == l1
+    assert all(torch.equal(a, b) for a, b in zip(g0, g1))
+    assert all(torch.equal(a, b) for a, b in zip(d0, d1))
