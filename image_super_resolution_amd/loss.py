@@ -40,9 +40,17 @@ class gen_loss:
         self.bce = nn.BCEWithLogitsLoss()
         self.beta = beta
 
-    def calc_contentLoss(self, sr_imgs: torch.Tensor, hr_imgs: torch.Tensor, sr_discriminated: torch.Tensor):
+    def calc_contentLoss(self, sr_imgs: torch.Tensor, hr_imgs: torch.Tensor, sr_discriminated: torch.Tensor,
+                         hr_features: torch.Tensor | None = None):
+        """`hr_features`: vgg_net(hr_imgs) computed ahead, or a callable returning it once ready
+        (trainer.train_srgan runs it on a second stream beside the D(sr) and VGG(sr) forwards);
+        None computes it here as the reference does."""
         sr_imgs_in_vgg_space = self.vgg_net(sr_imgs)
-        hr_imgs_in_vgg_space = self.vgg_net(hr_imgs).detach()
+        if hr_features is None:
+            hr_features = self.vgg_net(hr_imgs)
+        elif callable(hr_features):
+            hr_features = hr_features()
+        hr_imgs_in_vgg_space = hr_features.detach()
         content_loss = self.mse(sr_imgs_in_vgg_space, hr_imgs_in_vgg_space)
         adversarial_loss = self.bce(sr_discriminated, torch.ones_like(sr_discriminated))
         perceptual_loss = content_loss + self.beta * adversarial_loss

@@ -118,21 +118,37 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
     pending = []
     # the discriminator's forwards + backward on a second stream beside the generator's backward
     # (same results, tests/test_gpu_train_cfg3.py; A/B: ISR_TRAIN_D_OVERLAP=0)
-    overlap = os.environ.get("ISR_TRAIN_D_OVERLAP", "1") == "1"
+    # (not beside a persistent backward chain: its grid must own the chip, ISR_TRAIN_BWD_CHAIN)
+    overlap = (os.environ.get("ISR_TRAIN_D_OVERLAP", "1") == "1"
+               and os.environ.get("ISR_TRAIN_BWD_CHAIN", "0") != "1")
+    hr_overlap = overlap and os.environ.get("ISR_TRAIN_HR_OVERLAP", "1") == "1"
     d_stream = torch.cuda.Stream(device) if overlap and device.type == "cuda" else None
     for idx in range(total):
         hr_images, lr_images = transform(next(it))
         sr_images = gen_net(lr_images)
         sr_images = (sr_images + 1.0) / 2.0
         sr_images = (sr_images - mean) / std
+        hr_features = None
+        if d_stream is not None and hr_overlap:
+            # VGG(hr) on the second stream beside the D(sr) and VGG(sr) forwards; enqueued after the
+            # generator forward, whose persistent trunk grid must have the chip to itself
+            g_done = torch.cuda.Event()
+            g_done.record()
+            d_stream.wait_event(g_done)
+            with torch.cuda.stream(d_stream), torch.no_grad():
+                hr_features = compute_loss.vgg_net(hr_images)
         # the reference computes the discriminator's parameter gradients from the
         # generator loss and then discards them (optimizer_d.zero_grad, train.py:119);
         # D's parameters are frozen for this forward so only its input gradient is
         # computed — same parameter updates, one weight-gradient pass fewer
         with torch.autocast("cuda", dtype=torch.bfloat16), _frozen(dis_net):  # reference: fp16 autocast
             sr_discriminated = dis_net(sr_images)
-        perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(sr_images, hr_images,
-                                                                                         sr_discriminated)
+        if hr_features is not None:
+            perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(
+                sr_images, hr_images, sr_discriminated, hr_features=_joined(hr_features, d_stream))
+        else:
+            perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(sr_images, hr_images,
+                                                                                             sr_discriminated)
         optimizer_g.zero_grad(set_to_none=True)
         if d_stream is not None:
             fwd_done = torch.cuda.Event()
@@ -180,6 +196,16 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
             pending = []
     _verify(gen_net)
     return loss_g
+
+
+def _joined(t: torch.Tensor, side):
+    """A callable handing `t` (made on stream `side`) to the current stream once side's work is done."""
+    def get():
+        cur = torch.cuda.current_stream()
+        cur.wait_stream(side)
+        t.record_stream(cur)
+        return t
+    return get
 
 
 def _d_forward_backward(dis_net, compute_loss, sr_images, hr_images, optimizer_d, gradscaler_dis):

@@ -124,7 +124,8 @@ def test_cfg3_two_sample_slice_vs_oracle():
 
 def test_srgan_d_overlap_same_updates(monkeypatch):
     """train_srgan with the discriminator's forwards + backward on a second stream beside the
-    generator's backward (default) updates G and D exactly as the serial order (bit for bit)."""
+    generator's backward and VGG(hr) beside the D(sr) / VGG(sr) forwards (default) updates G and D
+    exactly as the serial order (bit for bit)."""
     def run(overlap):
         monkeypatch.setenv("ISR_TRAIN_D_OVERLAP", "1" if overlap else "0")
         torch.manual_seed(0)
