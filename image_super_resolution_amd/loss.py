@@ -43,9 +43,11 @@ class gen_loss:
     def calc_contentLoss(self, sr_imgs: torch.Tensor, hr_imgs: torch.Tensor, sr_discriminated: torch.Tensor,
                          hr_features: torch.Tensor | None = None):
         """`hr_features`: vgg_net(hr_imgs) computed ahead, or a callable returning it once ready
-        (trainer.train_srgan runs it on a second stream beside the D(sr) and VGG(sr) forwards);
-        None computes it here as the reference does."""
+        (trainer.train_srgan runs it on a second stream beside the VGG(sr) forward; `sr_discriminated`
+        may be such a callable too); None computes it here as the reference does."""
         sr_imgs_in_vgg_space = self.vgg_net(sr_imgs)
+        if callable(sr_discriminated):  # likewise made on a second stream (trainer.train_srgan)
+            sr_discriminated = sr_discriminated()
         if hr_features is None:
             hr_features = self.vgg_net(hr_imgs)
         elif callable(hr_features):

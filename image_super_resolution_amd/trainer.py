@@ -122,6 +122,7 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
     overlap = (os.environ.get("ISR_TRAIN_D_OVERLAP", "1") == "1"
                and os.environ.get("ISR_TRAIN_BWD_CHAIN", "0") != "1")
     hr_overlap = overlap and os.environ.get("ISR_TRAIN_HR_OVERLAP", "1") == "1"
+    dsr_side = hr_overlap and os.environ.get("ISR_TRAIN_DSR_SIDE", "1") == "1"
     d_stream = torch.cuda.Stream(device) if overlap and device.type == "cuda" else None
     for idx in range(total):
         hr_images, lr_images = transform(next(it))
@@ -135,15 +136,17 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
             g_done = torch.cuda.Event()
             g_done.record()
             d_stream.wait_event(g_done)
-            with torch.cuda.stream(d_stream), torch.no_grad():
-                hr_features = compute_loss.vgg_net(hr_images)
-        # the reference computes the discriminator's parameter gradients from the
-        # generator loss and then discards them (optimizer_d.zero_grad, train.py:119);
-        # D's parameters are frozen for this forward so only its input gradient is
-        # computed — same parameter updates, one weight-gradient pass fewer
-        with torch.autocast("cuda", dtype=torch.bfloat16), _frozen(dis_net):  # reference: fp16 autocast
-            sr_discriminated = dis_net(sr_images)
+            with torch.cuda.stream(d_stream):
+                if dsr_side:  # D(sr) too (VGG(sr) on the main stream beside both); its input-gradient
+                    # backward then runs on this stream too, autograd joining the streams
+                    sr_discriminated = _d_frozen_forward(dis_net, sr_images)
+                with torch.no_grad():
+                    hr_features = compute_loss.vgg_net(hr_images)
+        if hr_features is None or not dsr_side:
+            sr_discriminated = _d_frozen_forward(dis_net, sr_images)
         if hr_features is not None:
+            if dsr_side:
+                sr_discriminated = _joined(sr_discriminated, d_stream)
             perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(
                 sr_images, hr_images, sr_discriminated, hr_features=_joined(hr_features, d_stream))
         else:
@@ -196,6 +199,15 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
             pending = []
     _verify(gen_net)
     return loss_g
+
+
+def _d_frozen_forward(dis_net, sr_images):
+    """The reference computes the discriminator's parameter gradients from the generator loss and
+    then discards them (optimizer_d.zero_grad, train.py:119); D's parameters are frozen for this
+    forward so only its input gradient is computed — same parameter updates, one weight-gradient
+    pass fewer."""
+    with torch.autocast("cuda", dtype=torch.bfloat16), _frozen(dis_net):  # reference: fp16 autocast
+        return dis_net(sr_images)
 
 
 def _joined(t: torch.Tensor, side):
