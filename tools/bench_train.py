@@ -92,17 +92,38 @@ def main():
                           steps=n, log_every=10 ** 9)
     run(args.warmup)
     torch.cuda.synchronize()
-    if args.torch_profile:  # which PyTorch ops (copies / fills) a step issues, with call sites
-        from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+    if args.torch_profile:  # which PyTorch ops (copies / fills / adds) a step issues, with call sites
+        import collections
+        import traceback
+        from torch.utils._python_dispatch import TorchDispatchMode
+        keys = {"copy_", "fill_", "zero_", "clone", "add_", "add", "mul", "mul_", "sub", "div", "_to_copy", "cat",
+                "stack", "zeros_like", "ones_like", "where", "abs", "sum", "mean"}
+        root = str(Path(__file__).resolve().parents[1])
+
+        class _Count(TorchDispatchMode):
+            def __init__(self):
+                super().__init__()
+                self.n = collections.Counter()
+                self.bytes = collections.Counter()
+
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                name = func.overloadpacket.__name__
+                if name in keys:
+                    fr = [f for f in traceback.extract_stack()[:-1]
+                          if f.filename.startswith(root) and "bench_train" not in f.filename]
+                    site = " <- ".join(f"{Path(f.filename).name}:{f.lineno}" for f in fr[::-1][:3])
+                    a0 = args[0] if args and isinstance(args[0], torch.Tensor) else None
+                    self.n[(name, site)] += 1
+                    self.bytes[(name, site)] += 0 if a0 is None else a0.numel() * a0.element_size()
+                return func(*args, **(kwargs or {}))
+
+        mode = _Count()
+        with mode:
             run(args.steps)
             torch.cuda.synchronize()
-        keys = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::clone", "aten::add_", "aten::mul", "aten::sub",
-                "aten::add", "aten::div")
-        rows = sorted((e for e in prof.key_averages(group_by_stack_n=5) if e.key in keys), key=lambda e: -e.count)
-        for e in rows[:30]:
-            site = " <- ".join(f.strip().split(" ")[-1][-60:] for f in e.stack[:5])
-            print(f"{e.count / args.steps:7.1f}/step {e.key:14s} {site}")
+        for (name, site), c in sorted(mode.n.items(), key=lambda kv: -mode.bytes[kv[0]])[:40]:
+            print(f"{c / args.steps:7.1f}/step {mode.bytes[(name, site)] / args.steps / 2**20:10.1f} MiB/step "
+                  f"{name:10s} {site}")
         return
     if world > 1:
         torch.distributed.barrier()
