@@ -324,7 +324,9 @@ struct WgradGroupArgs {
     float* ws[WG_GROUP_MAX];
     int start[WG_GROUP_MAX + 1];   // wgrad blocks
     int rstart[WG_GROUP_MAX + 1];  // reduce blocks
-    int n, splits, tiles;
+    int pstart[WG_GROUP_MAX + 1];  // (co, ci) tile pairs
+    int n, splits, tiles, pairs;
+    int order;  // block order: 0 = member-major, 1 = split-major over all members' tile pairs
 };
 
 __device__ __forceinline__ int group_member(const WgradGroupArgs& g, const int* start, int b) {
@@ -334,11 +336,24 @@ __device__ __forceinline__ int group_member(const WgradGroupArgs& g, const int* 
     return t;
 }
 
+// Block order.  Member-major (0): conv t's blocks (ci tile, co tile, split) in turn, so an XCD's
+// contiguous share of the grid (xcd_remap) holds one or two members and each member re-reads the
+// dense buffer's channels it shares with the others.  Split-major (1): the blocks of one split —
+// one pixel range — over ALL members' tile pairs are adjacent, so the 26 blocks that read the same
+// pixel rows of the dense and gradient buffers run together on one XCD and share its L2.
 template <class C>
 __global__ __launch_bounds__(C::NT) void wgrad3x3_group_kernel(WgradGroupArgs g) {
-    const int b = xcd_remap(blockIdx.x, gridDim.x);
-    const int t = group_member(g, g.start, b);
-    wgrad_body<C>(g.d[t], g.ws[t], g.splits, g.tiles, b - g.start[t]);
+    const int l = xcd_remap(blockIdx.x, gridDim.x);
+    int t, b;
+    if (g.order == 1) {
+        const int split = l / g.pairs, p = l - split * g.pairs;
+        t = group_member(g, g.pstart, p);
+        b = (p - g.pstart[t]) + (g.pstart[t + 1] - g.pstart[t]) * split;
+    } else {
+        t = group_member(g, g.start, l);
+        b = l - g.start[t];
+    }
+    wgrad_body<C>(g.d[t], g.ws[t], g.splits, g.tiles, b);
 }
 
 // dW[co][ci][tap] (reference OIHW) = scale * sum_s ws[s][tap][co'][ci];  co' = kernel channel order.
@@ -663,16 +678,22 @@ static int group_plan(const isr_wgrad_desc* ds, int n, WgradGroupArgs* g, size_t
         off += ((size_t)splits * 9 * d.cout * d.cin + (size_t)splits * d.cout) * 4;
         off = (off + 255) / 256 * 256;
         g->start[t] = blk;
+        g->pstart[t] = blk / splits;
         blk += splits * (d.cout / C::CO_T) * (d.cin / C::CI_T);
         g->rstart[t] = rblk;
         rblk += (int)((((size_t)9 * d.cout * d.cin + d.cout) / 4 + 15) / 16);
     }
     g->start[n] = blk;
     g->rstart[n] = rblk;
-    for (int t = n + 1; t <= WG_GROUP_MAX; ++t) g->start[t] = g->rstart[t] = 0x7fffffff;
+    g->pstart[n] = pairs;
+    for (int t = n + 1; t <= WG_GROUP_MAX; ++t) g->start[t] = g->rstart[t] = g->pstart[t] = 0x7fffffff;
     g->n = n;
     g->splits = splits;
     g->tiles = tiles;
+    g->pairs = pairs;
+    // block order A/B (both give the same bits: every block's partial and the reduce are unchanged)
+    const char* e = getenv("ISR_WGRAD_GROUP_ORDER");
+    g->order = e ? atoi(e) : 1;
     *bytes = off;
     return 0;
 }

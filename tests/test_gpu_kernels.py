@@ -5,6 +5,8 @@ the remaining difference is fp32 accumulation order plus one bf16 rounding of
 the output: tolerance |err| <= 1.5e-2 * max(1, |ref|) elementwise, and mean
 error < 2e-3.
 """
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -370,6 +372,24 @@ def test_wgrad3x3_group_rdb_vs_autograd(n, h, w):
         ops.wgrad3x3(Db, cin, Eb, cout, dw1, db1, g_coff=gco, scale=sc)
         torch.cuda.synchronize()
         torch.testing.assert_close(dw, dw1, rtol=1e-5, atol=1e-5 * dw1.abs().max().item())
+    # the member-major block order (ISR_WGRAD_GROUP_ORDER=0) gives the same bits as the default
+    # split-major one: same blocks, same partials, same reduce
+    old = os.environ.get("ISR_WGRAD_GROUP_ORDER")
+    os.environ["ISR_WGRAD_GROUP_ORDER"] = "0"
+    try:
+        ref = [(dw.clone(), db.clone()) for dw, db in outs]
+        for dw, db in outs:
+            dw.fill_(float("nan"))
+            db.fill_(float("nan"))
+        assert lib.isr_wgrad3x3_group(arr, 5, ws.data_ptr(), ws.numel(), st) == 0
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("ISR_WGRAD_GROUP_ORDER")
+        else:
+            os.environ["ISR_WGRAD_GROUP_ORDER"] = old
+    for (dw, db), (rw, rb) in zip(outs, ref):
+        assert torch.equal(dw, rw) and torch.equal(db, rb)
     # a member on another computed grid (ha) is refused
     Ds = ops.ActBuffer.from_nchw(bf(_mk(n, 64, h + 64, w, 83)), pad=1)  # another computed extent
     bad = list(descs)
