@@ -1,6 +1,6 @@
 #!/bin/bash
-# Training steps on a high-priority stream (ISR_TRAIN_PRIO=1): training tests with it on, then a
-# same-box A/B of the cfg3 step, alternating processes.
+# Training steps on a high-priority stream (ISR_TRAIN_PRIO=1, option since removed: 65 vs 46 ms,
+# profiles/r04_train_prio_ab.jsonl): training tests with it on, then a same-box A/B, alternating.
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/r04
