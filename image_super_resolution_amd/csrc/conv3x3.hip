@@ -181,11 +181,15 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
         const int sj = (lane / CG) & 1;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
+            // registers 4j..4j+3 are 4 consecutive couts (the 4 sub-pixels of one shuffled
+            // channel): one 16-byte write each (lane units 17·l31 + 2j + hh: conflict-free)
 #pragma unroll
             for (int f = 0; f < NF; ++f)
 #pragma unroll
-                for (int g = 0; g < 16; ++g)
-                    ep[l31 * EPS + f * 32 + (g & 3) + 8 * (g >> 2) + 4 * hh] = acc[r][f][g];
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 q = {acc[r][f][4 * j], acc[r][f][4 * j + 1], acc[r][f][4 * j + 2], acc[r][f][4 * j + 3]};
+                    *reinterpret_cast<f32x4*>(ep + l31 * EPS + f * 32 + 8 * j + 4 * hh) = q;
+                }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
             const int yy = y0 + wave * R + r;
