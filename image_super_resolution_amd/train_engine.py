@@ -537,6 +537,9 @@ class GeneratorTrainPlan:
             rc = e[0](byref(e[1]), st)
             if rc != 0:
                 ops.check(rc, "train forward")
+            if self.chain is not None and e[1] is self.chain.desc:
+                self.trunk_done = torch.cuda.Event()
+                self.trunk_done.record()
         if self.chain is not None:
             self.chain.poll()  # lagged, non-blocking give-up check (engine.ConvChain.poll)
         if self.bn_counters:
@@ -778,12 +781,19 @@ def _device_shared() -> bool:
     return dist.get_backend() == "gloo" or local > max(1, torch.cuda.device_count())
 
 
+def _plan_of(gen: nn.Module):
+    """The training plan of a generator (an SRGAN's lives on its res_net, where train_forward runs)."""
+    from .models import SRGAN
+    if isinstance(gen, SRGAN):
+        gen = gen.res_net
+    return gen.__dict__.get("_isr_train_plan")
+
+
 def verify_chains(gen: nn.Module) -> None:
     """Blocking persistent-chain give-up check of every training forward queued so far on this
     generator (engine.ChainFailed); the trainer calls it at the end of every epoch, before the
     epoch's results (losses, checkpoint) are handed out."""
-    plan = gen.__dict__.get("_isr_train_plan")
-    chain = getattr(plan, "chain", None)  # the Denoise training plan has no trunk chain
+    chain = getattr(_plan_of(gen), "chain", None)  # the Denoise training plan has no trunk chain
     if chain is not None:
         chain.verify()
 
@@ -791,9 +801,15 @@ def verify_chains(gen: nn.Module) -> None:
 def step_guard_ptr(gen: nn.Module):
     """The trunk give-up guard of the generator's last training forward (engine.ConvChain.guard_ptr),
     or None when it ran without the persistent trunk kernel."""
-    plan = gen.__dict__.get("_isr_train_plan")
-    chain = getattr(plan, "chain", None)
+    chain = getattr(_plan_of(gen), "chain", None)
     return chain.guard_ptr if chain is not None else None
+
+
+def trunk_done_event(gen: nn.Module):
+    """An event recorded on the forward's stream right after its persistent trunk kernel (None
+    without one): work that must not run beside that grid may be queued behind it."""
+    plan = _plan_of(gen)
+    return getattr(plan, "trunk_done", None) if getattr(plan, "chain", None) is not None else None
 
 
 def get_train_plan(gen: nn.Module, x: torch.Tensor) -> GeneratorTrainPlan:

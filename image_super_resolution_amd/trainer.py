@@ -37,7 +37,7 @@ import torch
 from .models import ModelEMA
 from .optim import clip_grad_norm_  # HIP multi-tensor clip (same signature as torch's)
 from .optim import step_guard
-from .train_engine import allreduce_grads, step_guard_ptr
+from .train_engine import allreduce_grads, step_guard_ptr, trunk_done_event
 
 
 def _scalar(writer, tag, value, step):
@@ -123,6 +123,7 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
                and os.environ.get("ISR_TRAIN_BWD_CHAIN", "0") != "1")
     hr_overlap = overlap and os.environ.get("ISR_TRAIN_HR_OVERLAP", "1") == "1"
     dsr_side = hr_overlap and os.environ.get("ISR_TRAIN_DSR_SIDE", "1") == "1"
+    hr_early = hr_overlap and os.environ.get("ISR_TRAIN_HR_EARLY", "1") == "1"
     d_stream = torch.cuda.Stream(device) if overlap and device.type == "cuda" else None
     for idx in range(total):
         hr_images, lr_images = transform(next(it))
@@ -135,13 +136,16 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
             # generator forward, whose persistent trunk grid must have the chip to itself
             g_done = torch.cuda.Event()
             g_done.record()
-            d_stream.wait_event(g_done)
+            # VGG(hr) needs only the trunk kernel to be done (not the upsampler / tail after it)
+            t_done = trunk_done_event(_unwrap(gen_net)) if hr_early else None
+            d_stream.wait_event(t_done if t_done is not None else g_done)
             with torch.cuda.stream(d_stream):
-                if dsr_side:  # D(sr) too (VGG(sr) on the main stream beside both); its input-gradient
-                    # backward then runs on this stream too, autograd joining the streams
-                    sr_discriminated = _d_frozen_forward(dis_net, sr_images)
                 with torch.no_grad():
                     hr_features = compute_loss.vgg_net(hr_images)
+                if dsr_side:  # D(sr) too (VGG(sr) on the main stream beside both); its input-gradient
+                    # backward then runs on this stream too, autograd joining the streams
+                    d_stream.wait_event(g_done)
+                    sr_discriminated = _d_frozen_forward(dis_net, sr_images)
         if hr_features is None or not dsr_side:
             sr_discriminated = _d_frozen_forward(dis_net, sr_images)
         if hr_features is not None:

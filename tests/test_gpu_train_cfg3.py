@@ -58,6 +58,8 @@ def _srgan_step_grads(chain: bool, dis, gl):
         torch.cuda.synchronize()
         plan = gen.res_net.__dict__["_isr_train_plan"]
         assert (plan.chain is not None) == chain, "trunk kernel on/off as requested"
+        # the SRGAN wrapper's step is guarded by its res_net's trunk give-up count
+        assert (trainer.step_guard_ptr(gen) is not None) == chain
         return losses[0], {n: p.grad.detach().clone() for n, p in gen.named_parameters()}
     finally:
         if old is None:
