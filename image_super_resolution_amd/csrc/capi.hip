@@ -253,11 +253,17 @@ int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_
     if (variant == 0 || (variant >= 2 && variant <= 8)) {
         static const int form_of[9] = {0, 0, 1, 2, 3, 4, 5, 6, 7};
         const int rc = isr::trunk_launch(c, (hipStream_t)s, form_of[variant]);
+        if (rc == -3) return fail(ISR_ERR_UNSUPPORTED, "conv chain: variant %d is an A/B form of the tuning library "
+                                  "(lib/libisr_tuning.so)", variant);
         if (rc == -4) return fail(ISR_ERR_LAUNCH, "conv chain: the occupancy query admits no workgroup per CU");
         if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "conv chain: unsupported grid or layer count");
         return launched(rc, "conv chain");
     }
-    if (variant == 1) return launched(isr::conv_chain(c, (hipStream_t)s), "conv chain (round-2 kernel)");
+    if (variant == 1) {
+        const int rc = isr::conv_chain(c, (hipStream_t)s);
+        if (rc == -3) return fail(ISR_ERR_UNSUPPORTED, "conv chain: variant 1 (the round-2 kernel) is in the tuning library only");
+        return launched(rc, "conv chain (round-2 kernel)");
+    }
     return fail(ISR_ERR_UNSUPPORTED, "conv chain: unknown variant %d", variant);
 }
 

@@ -764,12 +764,13 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
     if (d->cout % 64) {  // 32-cout tiles: growth convs (cout 32) and dgrad of them (96, 160)
         switch (variant) {
             case 0: return launch3x3<V_G0, true>(d, s);
+#ifdef ISR_TUNING
+            // A/B tile configurations (none faster than V_G0 on the generator's shapes)
             case 1: return launch3x3<V_G1>(d, s);
             case 2: return launch3x3<V_G2>(d, s);
             case 3: return launch3x3<V_G3>(d, s);
             case 8: return launch3x3<C3<4, 4, 1, 16, 2, 0, 0, 2, 4, 1>>(d, s);  // V_G0, refill before step-0 reads (r1)
             case 9: return launch3x3<C3<4, 8, 1, 16, 2, 0, 0, 2>>(d, s);  // 32x32 tile, 8 waves, PIPE 2 (92 KB, 1 block/CU)
-#ifdef ISR_TUNING
             // ablations of V_G0 (timing only, outputs wrong): tuning builds only
             case 4: return launch3x3<C3<4, 4, 1, 16, 2, 0, 1>>(d, s);
             case 5: return launch3x3<C3<4, 4, 1, 16, 2, 0, 2>>(d, s);
@@ -782,6 +783,7 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
     switch (variant) {
         case 0: return d->cin == 192 ? (fold_host(d) ? launch3x3<V_F0F>(d, s) : launch3x3<V_F0, true>(d, s))
                                      : launch3x3<V_W0, true>(d, s);
+#ifdef ISR_TUNING
         case 1: return launch3x3<V_W1>(d, s);
         case 2: return launch3x3<V_W2>(d, s);
         case 3: return launch3x3<V_W3>(d, s);
@@ -789,7 +791,6 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 2, 4, 1>>(d, s);
         case 9: return d->cin == 192 ? launch3x3<C3<4, 8, 2, 16, 2, 192, 0, 2>>(d, s)  // 32x32, 8 waves, PIPE 2 (111 KB)
                                      : launch3x3<C3<4, 8, 2, 16, 2, 0, 0, 2>>(d, s);
-#ifdef ISR_TUNING
         // ablations of V_W0 (timing only, outputs wrong): tuning builds only
         case 4: return launch3x3<C3<4, 4, 2, 16, 2, 0, 1>>(d, s);
         case 5: return launch3x3<C3<4, 4, 2, 16, 2, 0, 2>>(d, s);
@@ -861,6 +862,9 @@ __device__ __forceinline__ void chain_tuning_prologue(int ntiles) {
 #endif
 }
 
+// The round-2 per-tile chain kernel (isr_conv_chain variant 1): superseded by trunk.hip, kept in the
+// tuning library only (-DISR_TUNING).
+#ifdef ISR_TUNING
 __global__ void chain_bump_kernel(unsigned* state) {
     if (threadIdx.x == 0) state[threadIdx.x] = state[threadIdx.x] + 1u;  // vector store by lane 0
 }
@@ -977,10 +981,6 @@ __global__ __launch_bounds__(CG::NT, 2) void conv_chain_kernel(ChainArgs a) {
     if (pend_t >= 0) publish_pending();
 }
 
-size_t conv_chain_state_words(int n, int ha, int wa) {
-    const size_t tiles = (size_t)n * (ha / V_G0::TH) * (wa / V_G0::TW);
-    return (tiles + 4 + 3) / 4 * 4;  // [0] fail word, [4..] progress; a multiple of 16 bytes
-}
 
 #ifdef ISR_TUNING
 static int g_chain_variant_host = 0;  // isr_tuning_chain_knobs k2: chain kernel variant (A/B only)
@@ -1043,6 +1043,15 @@ int conv_chain(const isr_chain_desc* c, hipStream_t s) {
     // three dependent scalar round trips, ~2.4 µs per tile — overlap the wait): -1.2 % per
     // forward against waiting first (tools/chain_probe.py, variant 0 vs 5)
     return launch_chain<V_G0, V_F0F, 1>(c, s);
+}
+
+#else
+int conv_chain(const isr_chain_desc*, hipStream_t) { return -3; }
+#endif  // ISR_TUNING (round-2 chain)
+
+size_t conv_chain_state_words(int n, int ha, int wa) {
+    const size_t tiles = (size_t)n * (ha / V_G0::TH) * (wa / V_G0::TW);
+    return (tiles + 4 + 3) / 4 * 4;  // [0] fail word, [4..] progress; a multiple of 16 bytes
 }
 
 #ifdef ISR_TUNING

@@ -171,6 +171,7 @@ static_assert(TR * HC % 32 == 0, "");
 
 // packed tail weights: [kx 9][chunk 2][ks 2][n 32][hpos 2][8] bf16,
 // n = ky*3 + co (27 used), element = W[co][chunk*32 + ks*16 + h*8 + e][ky][kx], h = hpos ^ ((n>>3)&1).
+#ifdef ISR_TUNING  // variant 1 (the 16-row per-tile kernel): tuning library only
 __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
     using namespace tail;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -270,6 +271,8 @@ __global__ __launch_bounds__(256) void tail9x9_kernel(isr_tail_desc d) {
         }
     }
 }
+
+#endif
 
 // ---- 8-row tail (variant 3): the per-tile kernel with 8 output rows per block and one
 // 32-channel halo chunk resident at a time (chunk 1 refills chunk 0's slot after a
@@ -1272,6 +1275,12 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
     // walk (4) and 236-280 us for the lane-streaming walk (6), all bit-identical
     // (tools/tune_tail.py, tests/test_gpu_kernels.py); the persistent variant 2 measures 515 us
     if (variant == 0) variant = 5;
+#ifndef ISR_TUNING
+    // production: the row-streaming walk (5) and the 8-row per-tile kernel (3, the fallback of
+    // images whose fp32 output passes 2 GiB); the other forms are in the tuning library only
+    if (variant != 3 && variant != 5) return -2;
+#endif
+#ifdef ISR_TUNING
     if (variant == 2 || (variant >= 10 && variant <= 17)) {  // persistent
         const int cus = cu_count();
         const int ntiles = d->n * (d->ha / tail::TH) * (d->wa / tail::TW);
@@ -1289,7 +1298,8 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             default: return go(tail9x9_pkernel<0>);
         }
     }
-    int abl = 0, lane_sh = 0;
+#endif
+    [[maybe_unused]] int abl = 0, lane_sh = 0;
 #ifdef ISR_TUNING
     if (variant >= 20 && variant < 70) {  // 20 + ABL: stream-tail ablations
         abl = variant - 20;
@@ -1314,6 +1324,7 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
     }
 #endif
     if ((variant == 4 || variant == 5 || variant == 6) && (size_t)3 * d->h * d->w * (d->y_u8 ? 1 : 4) >= ((size_t)1 << 31)) variant = 3;  // 32-bit store offsets
+#ifdef ISR_TUNING
     if (variant == 6) {
         int sh = lane_sh;
         if (sh == 0) {
@@ -1340,6 +1351,7 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             default: return go(tail9x9_lane_kernel<0>);
         }
     }
+#endif
     if (variant == 5) {
         // segment height: the longest walk (<= 512 rows) that still gives every CU a strip —
         // fewer, longer walks recompute fewer halo T rows and leave no partial last wave of
@@ -1371,6 +1383,7 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             default: return go(tail9x9_stream8_kernel<0>);
         }
     }
+#ifdef ISR_TUNING
     if (variant == 4) {
         // segment height: 8 T rows per segment are recomputed by the neighbour (6 % at 128)
         int sh = 128;
@@ -1401,17 +1414,22 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             default: return go(tail9x9_stream_kernel<0>);
         }
     }
+#endif
     if (variant == 3) {
         lds_limit((const void*)tail9x9_k8_kernel, tail8::LDS);
         dim3 grid8(d->wa / tail8::TW, d->ha / tail8::TH, d->n);
         hipLaunchKernelGGL(tail9x9_k8_kernel, grid8, dim3(256), tail8::LDS, s, *d);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
+#ifdef ISR_TUNING
     if (variant != 1) return -2;
     lds_limit((const void*)tail9x9_kernel, tail::LDS);
     dim3 grid(d->wa / tail::TW, d->ha / tail::TH, d->n);
     hipLaunchKernelGGL(tail9x9_kernel, grid, dim3(256), tail::LDS, s, *d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+#else
+    return -2;
+#endif
 }
 
 #ifdef ISR_TUNING

@@ -997,6 +997,11 @@ static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
 // 7.77 ms for the deep form (same box, tools/ab_chain.py, profiles/r03_ab_chain.jsonl) — the deep
 // form's 2-row waves read 7 LDS fragments per 6 MFMAs (4-row waves: 9 per 12)
 using TK_PAIR = TK<4, 4, 2>;
+
+// The A/B forms below measured slower than the pair form on the same boxes and are
+// compiled only into the tuning library (-DISR_TUNING, lib/libisr_tuning.so): the production
+// libisr.so carries the production form alone.
+#ifdef ISR_TUNING
 using TK_DEEP = TK<8, 2, 4>;   // one 8-wave workgroup per CU, 3 chunks in flight
 // 32x32 tiles: one 8-wave workgroup per CU (4 rows per wave, as the pair form), the chunk's
 // weights staged once per CU instead of twice and a (34x34)/(32x32) halo instead of (18x34)/(16x32)
@@ -1010,15 +1015,20 @@ using TK_PAIR_NTS = TK<4, 4, 2, 16, 0, 2>;  // non-temporal output stores
 
 int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_deep.hip
 int trunk_deep_knobs_set(const int* k);
+#endif
 
 int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
+    if (form == 0) return trunk_launch_k<TK_PAIR>(cd, s);
+#ifdef ISR_TUNING
     if (form == 3) return trunk_deep_launch(cd, s);
     if (form == 2) return trunk_launch_k<TK_T32>(cd, s);
     if (form == 4) return trunk_launch_k<TK_QUAD>(cd, s);
     if (form == 5) return trunk_launch_k<TK_PAIR_X>(cd, s);
     if (form == 6) return trunk_launch_k<TK_PAIR_NTH>(cd, s);
     if (form == 7) return trunk_launch_k<TK_PAIR_NTS>(cd, s);
-    return form == 1 ? trunk_launch_k<TK_DEEP>(cd, s) : trunk_launch_k<TK_PAIR>(cd, s);
+    if (form == 1) return trunk_launch_k<TK_DEEP>(cd, s);
+#endif
+    return -3;  // an A/B form of the tuning library
 }
 
 #ifdef ISR_TUNING

@@ -36,6 +36,9 @@
 
 namespace isr {
 
+// An A/B form (7.54 vs 6.36 ms per forward): compiled into the tuning library only.
+#ifdef ISR_TUNING
+
 namespace td {
 constexpr int TH = 32, TW = 32, WM = 8, R = 4, NT = 64 * WM;
 constexpr int HC = TW + 2, HQ = (TH + 2) * HC;  // 34 x 34 halo pixels
@@ -833,7 +836,6 @@ int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-#ifdef ISR_TUNING
 int trunk_deep_knobs_set(const int* k) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_trunkd_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
 }
@@ -849,9 +851,7 @@ int trunk_deep_stats(unsigned long long* out, int reset) {
     return 0;
 }
 #else
-int trunk_deep_knobs_set(const int*) { return -2; }
 int trunk_deep_stats(unsigned long long*, int) { return -2; }
-int trunk_deep_stamps_set(void*) { return -2; }
 #endif
 
 }  // namespace isr

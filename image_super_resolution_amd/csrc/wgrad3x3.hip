@@ -691,9 +691,13 @@ static int group_plan(const isr_wgrad_desc* ds, int n, WgradGroupArgs* g, size_t
     g->splits = splits;
     g->tiles = tiles;
     g->pairs = pairs;
-    // block order A/B (both give the same bits: every block's partial and the reduce are unchanged)
-    const char* e = getenv("ISR_WGRAD_GROUP_ORDER");
-    g->order = e ? atoi(e) : 1;
+    // block order: split-major (1) in production; the pair-major A/B form (0) only in tuning
+    // builds (both give the same bits: every block's partial and the reduce are unchanged)
+    g->order = 1;
+#ifdef ISR_TUNING
+    static const int order_probe = getenv("ISR_WGRAD_GROUP_ORDER") ? atoi(getenv("ISR_WGRAD_GROUP_ORDER")) : 1;
+    g->order = order_probe;
+#endif
     *bytes = off;
     return 0;
 }

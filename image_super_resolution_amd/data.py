@@ -149,12 +149,74 @@ class NoisyTransform:
         return hr.contiguous(), lr.contiguous()
 
 
-class SyntheticSR:
-    """Endless synthetic uint8 HR crops on the GPU: bicubic-upsampled 32x32
-    uniform noise (a smooth 'natural-ish' image), seed per batch and rank."""
+NATURAL_ALPHA = 1.4  # amplitude spectrum 1/f^alpha: x4 bicubic PSNR ~27.7 dB, the regime of COCO crops
 
-    def __init__(self, batch: int, target_size: int, seed: int = 0, device="cuda"):
-        self.batch, self.t, self.seed, self.device = batch, target_size, seed, device
+
+def natural_hr_u8(n: int, t: int, generator: torch.Generator, device="cuda", alpha: float = NATURAL_ALPHA,
+                  contrast: float = 0.25) -> torch.Tensor:
+    """uint8 [n, 3, t, t] Gaussian fields with a natural-image power spectrum.
+
+    White noise (a luma field shared by the channels plus 0.35x independent colour noise) shaped
+    by 1/f^alpha in the Fourier domain, unit standard deviation per image, mapped to
+    0.5 + contrast*x and clipped to [0, 1].  At alpha = 1.4 the x4 task is as hard as natural
+    photos are for bicubic upsampling (about 27.7 dB PSNR on the cv2 LR of train.py), unlike the
+    smooth kind, where bicubic already reaches ~46 dB and the last bf16 bits never matter."""
+    w = torch.randn(n, 3, t, t, generator=generator, device=device)
+    luma = torch.randn(n, 1, t, t, generator=generator, device=device)
+    w = 0.35 * w + luma
+    fy = torch.fft.fftfreq(t, device=device).view(-1, 1)
+    fx = torch.fft.rfftfreq(t, device=device).view(1, -1)
+    f = torch.sqrt(fx * fx + fy * fy).clamp_min(1.0 / t)
+    x = torch.fft.irfft2(torch.fft.rfft2(w) / f.pow(alpha), s=(t, t))
+    x = x / x.flatten(1).std(1).view(-1, 1, 1, 1)
+    return (0.5 + contrast * x).clamp_(0, 1).mul_(255).round_().to(torch.uint8)
+
+
+def leaves_hr_u8(n: int, t: int, generator: torch.Generator, device="cuda", discs: int = 500, rmin: float = 4.0,
+                  contrast: float = 0.6, texture: float = 0.3) -> torch.Tensor:
+    """uint8 [n, 3, t, t] 'dead leaves' images: the standard synthetic model of natural-image
+    statistics (occluding objects with a power-law size distribution give sharp edges and a
+    1/f-like spectrum), plus a 1/f^1.4 texture (natural_hr_u8) on top.
+
+    `discs` opaque discs per image, front to back: centre uniform over the image, radius
+    r ~ r^-3 on [rmin, t/3], a uniform random RGB colour; every pixel shows the first disc that
+    covers it (grey where none does); colours enter as 0.5 + contrast*(c - 0.5), the texture as
+    texture*(its [0, 1] value - 0.5).  x4 bicubic on these reaches ~27 dB, a trained x4 RRDB
+    generator a few dB more (edges are what SR recovers; a Gaussian field has none)."""
+    ys = torch.arange(t, dtype=torch.float32, device=device).view(1, t, 1)
+    xs = torch.arange(t, dtype=torch.float32, device=device).view(1, 1, t)
+    rmax, a1 = t / 3.0, -2.0  # 1 - alpha for alpha = 3
+    out = torch.empty(n, 3, t, t, device=device)
+    for i in range(n):
+        cy = torch.rand(discs, generator=generator, device=device) * t
+        cx = torch.rand(discs, generator=generator, device=device) * t
+        u = torch.rand(discs, generator=generator, device=device)
+        r2 = ((rmin ** a1 + u * (rmax ** a1 - rmin ** a1)) ** (1.0 / a1)) ** 2
+        col = 0.5 + contrast * (torch.rand(discs, 3, generator=generator, device=device) - 0.5)
+        top = torch.full((t, t), discs, dtype=torch.long, device=device)  # index of the top disc
+        for j0 in range(0, discs, 64):  # front to back: a pixel keeps the first disc that covers it
+            sl = slice(j0, min(j0 + 64, discs))
+            inside = (ys - cy[sl].view(-1, 1, 1)) ** 2 + (xs - cx[sl].view(-1, 1, 1)) ** 2 <= r2[sl].view(-1, 1, 1)
+            first = inside.to(torch.uint8).argmax(0) + j0
+            top = torch.where(inside.any(0) & (top == discs), first, top)
+        pal = torch.cat([col, torch.full((1, 3), 0.5, device=device)])
+        out[i] = pal[top].permute(2, 0, 1)
+    tex = natural_hr_u8(n, t, generator, device).float().div_(255.0).sub_(0.5)
+    return (out + texture * tex).clamp_(0, 1).mul_(255).round_().to(torch.uint8)
+
+
+class SyntheticSR:
+    """Endless synthetic uint8 HR crops on the GPU, seed per batch and rank.
+
+    kind "smooth": bicubic-upsampled 32x32 uniform noise (a smooth 'natural-ish' image);
+    kind "natural": 1/f^1.4 Gaussian fields (natural_hr_u8);
+    kind "leaves": dead-leaves images with a 1/f texture (leaves_hr_u8), the data the committed
+    trained weights (tests/golden/trained_resnet_x4.safetensors) were made from."""
+
+    def __init__(self, batch: int, target_size: int, seed: int = 0, device="cuda", kind: str = "smooth"):
+        if kind not in ("smooth", "natural", "leaves"):
+            raise ValueError(f"SyntheticSR kind {kind!r}: 'smooth', 'natural' or 'leaves'")
+        self.batch, self.t, self.seed, self.device, self.kind = batch, target_size, seed, device, kind
         self.i = 0
 
     def __iter__(self):
@@ -163,6 +225,10 @@ class SyntheticSR:
     def __next__(self) -> torch.Tensor:
         g = torch.Generator(device=self.device).manual_seed(self.seed * 1_000_003 + self.i)
         self.i += 1
+        if self.kind == "natural":
+            return natural_hr_u8(self.batch, self.t, g, self.device)
+        if self.kind == "leaves":
+            return leaves_hr_u8(self.batch, self.t, g, self.device)
         base = torch.rand(self.batch, 3, 32, 32, generator=g, device=self.device)
         hr = F.interpolate(base, size=(self.t, self.t), mode="bicubic", align_corners=False).clamp_(0, 1)
         return (hr * 255).round_().to(torch.uint8)

@@ -389,8 +389,16 @@ def _gather_host(mine, done, s, canvas_shape, rank, world, group):
         canvas = torch.zeros(canvas_shape, dtype=torch.uint8)
         copy_tiles_to_host(mine, done, s, canvas)
         return canvas
+    import socket
     import tempfile
     import torch.distributed as dist
+    # one shared /dev/shm canvas needs every rank on rank 0's node: refuse otherwise (every
+    # rank gets the same verdict, so none is left waiting in a collective)
+    hosts = [None] * world
+    dist.all_gather_object(hosts, socket.gethostname(), group=group)
+    if len(set(hosts)) != 1:
+        raise RuntimeError(f"gather='host' needs every rank on one node (ranks on {sorted(set(hosts))}); "
+                           "use gather='device'")
     name = [None]
     if rank == 0:
         fd, name[0] = tempfile.mkstemp(prefix="isr_canvas_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
@@ -398,9 +406,17 @@ def _gather_host(mine, done, s, canvas_shape, rank, world, group):
         np.memmap(name[0], dtype=np.uint8, mode="w+", shape=canvas_shape).flush()  # sized, zero-filled
     dist.broadcast_object_list(name, src=0, group=group)
     try:
-        mm = np.memmap(name[0], dtype=np.uint8, mode="r+", shape=canvas_shape)
-        copy_tiles_to_host(mine, done, s, torch.from_numpy(mm))
-        dist.barrier(group=group)  # every rank's tiles are in the canvas
+        err = None
+        try:
+            mm = np.memmap(name[0], dtype=np.uint8, mode="r+", shape=canvas_shape)
+            copy_tiles_to_host(mine, done, s, torch.from_numpy(mm))
+        except Exception as e:  # reported to every rank below instead of leaving rank 0 waiting
+            err = f"rank {rank}: {type(e).__name__}: {e}"
+        errs = [None] * world
+        dist.all_gather_object(errs, err, group=group)  # also the "every rank's tiles are in" barrier
+        bad = [e for e in errs if e is not None]
+        if bad:
+            raise RuntimeError("gather='host' failed: " + "; ".join(bad))
         out = torch.from_numpy(mm) if rank == 0 else None  # rank 0 keeps the mapping (no copy)
     finally:
         if rank == 0:

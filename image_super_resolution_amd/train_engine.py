@@ -789,20 +789,65 @@ def _plan_of(gen: nn.Module):
     return gen.__dict__.get("_isr_train_plan")
 
 
+def _grad_group(gen: nn.Module):
+    """The process group of the generator's gradient all-reduce (enable_grad_allreduce), or None."""
+    from .models import SRGAN
+    if isinstance(gen, SRGAN):
+        gen = gen.res_net
+    return gen.__dict__.get("_isr_grad_group")
+
+
 def verify_chains(gen: nn.Module) -> None:
     """Blocking persistent-chain give-up check of every training forward queued so far on this
     generator (engine.ChainFailed); the trainer calls it at the end of every epoch, before the
-    epoch's results (losses, checkpoint) are handed out."""
+    epoch's results (losses, checkpoint) are handed out.  Data parallel: every rank raises when
+    any rank's trunk gave up (one all-reduce of the local verdict), so no rank walks on into a
+    collective its failed peer will never join."""
+    from .engine import ChainFailed
     chain = getattr(_plan_of(gen), "chain", None)  # the Denoise training plan has no trunk chain
-    if chain is not None:
+    if chain is None:
+        return
+    group = _grad_group(gen)
+    if group is None:
         chain.verify()
+        return
+    try:
+        chain.verify()
+        bad = 0
+    except ChainFailed:
+        bad = 1
+    t = torch.tensor([bad], dtype=torch.int32, device=chain.state.device)
+    all_reduce_(t, None if group is True else group)
+    if int(t.item()):
+        raise ChainFailed(f"conv chain: a dependency wait gave up on {int(t.item())} rank(s); the "
+                          "affected steps were skipped on every rank")
 
 
 def step_guard_ptr(gen: nn.Module):
     """The trunk give-up guard of the generator's last training forward (engine.ConvChain.guard_ptr),
-    or None when it ran without the persistent trunk kernel."""
-    chain = getattr(_plan_of(gen), "chain", None)
-    return chain.guard_ptr if chain is not None else None
+    or None when it ran without the persistent trunk kernel.
+
+    Data parallel (enable_grad_allreduce): the gradients are already averaged over the ranks when
+    the guard is read, so a rank whose trunk gave up has mixed invalid gradients into every peer's.
+    The guard is therefore global: each rank's "gave up and not yet reported" flag
+    (state[2] != state[3]) is summed over the group on the device and written into a two-word
+    guard [sum, 0] that every rank's guarded Adam / EMA kernels read — all ranks skip the step
+    together and the replicas stay identical.  Called once per step on every rank (one small
+    all-reduce, no host synchronisation with RCCL)."""
+    plan = _plan_of(gen)
+    chain = getattr(plan, "chain", None)
+    if chain is None:
+        return None
+    group = _grad_group(gen)
+    if group is None:
+        return chain.guard_ptr
+    g = plan.__dict__.get("_global_guard")
+    if g is None:
+        g = plan.__dict__["_global_guard"] = torch.zeros(2, dtype=torch.int32, device=chain.state.device)
+    flag = (chain.state[2:3] != chain.state[3:4]).to(torch.int32)
+    all_reduce_(flag, None if group is True else group)
+    g[0:1].copy_(flag)
+    return g.data_ptr()
 
 
 def trunk_done_event(gen: nn.Module):

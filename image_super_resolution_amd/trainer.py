@@ -21,7 +21,14 @@ Differences, all deliberate:
   every iteration (train.py:64-65, :101-112).
 * a forward whose persistent trunk kernel gave up (engine.ChainFailed, reported at the latest
   at epoch end) changes no parameter: every Adam / EMA update of that step and of later steps
-  is skipped on the device (optim.step_guard) until the host has reported the failure.
+  is skipped on the device (optim.step_guard) until the host has reported the failure.  Under
+  data parallelism the guard is global (train_engine.step_guard_ptr: the give-up flags are
+  summed over the ranks before the optimiser runs), so every rank skips together and every
+  rank raises at epoch end.  What a skipped step still advances: the host-side counters
+  (FusedAdam's per-parameter step used for bias correction, ModelEMA.updates, the LR
+  schedules) and the discriminator's BatchNorm running statistics (its train-mode forwards ran
+  on the invalid sr images).  ChainFailed means "this epoch's results are void": resume from
+  the last checkpoint rather than from the in-memory state.
 * multi-GPU (one process per GPU): the generator's gradients are averaged by
   one RCCL all-reduce of its flat gradient buffer inside the HIP backward
   (train_engine.enable_grad_allreduce); the discriminator's by one flat

@@ -87,3 +87,29 @@ def normalize(x01: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD) -> torch.
     m = torch.tensor(mean, dtype=x01.dtype, device=x01.device).view(1, 3, 1, 1)
     s = torch.tensor(std, dtype=x01.dtype, device=x01.device).view(1, 3, 1, 1)
     return (x01 - m) / s
+
+
+HELDOUT_SEED = 20_251_018  # never used by train.py's synthetic stream (seed*1_000_003 + i, seed = 100*131 + rank)
+
+
+def heldout_tiles(n: int, lr_size: int = 128, scale: int = 4, seed: int = HELDOUT_SEED, device="cpu",
+                  mean=IMAGENET_MEAN, std=IMAGENET_STD) -> tuple[torch.Tensor, torch.Tensor]:
+    """Held-out tiles of the `leaves` synthetic distribution the committed trained weights were
+    trained on (data.leaves_hr_u8: dead-leaves images with a 1/f texture).
+
+    Tile i is drawn from its own generator (seed + i) on `device`, so it does not depend on n (the
+    values do depend on the device's RNG: CPU and GPU tiles differ, each is reproducible).  HR:
+    uint8 images of side lr_size*scale; LR: train.py's transform of them (cv2 INTER_LINEAR resize
+    of the uint8 crop, rounded half up, then Normalize — data.GPUTransform's formula,
+    utils/datasets.py:302-304).  Returns (lr normalised fp32 [n,3,h,w], hr in [0,1] fp32
+    [n,3,h*scale,w*scale]), on the CPU."""
+    import torch.nn.functional as F
+
+    from .data import leaves_hr_u8
+    t = lr_size * scale
+    hr_u8 = torch.cat([leaves_hr_u8(1, t, torch.Generator(device=device).manual_seed(seed + i), device)
+                       for i in range(n)]).cpu()
+    x255 = hr_u8.float()
+    lr = F.interpolate(x255, size=(lr_size, lr_size), mode="bilinear", align_corners=False, antialias=False)
+    lr = (lr + 0.5).floor_().div_(255.0)
+    return normalize(lr, mean, std).contiguous(), (x255 / 255.0).contiguous()

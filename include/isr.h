@@ -340,11 +340,11 @@ int isr_pack_tail9x9(const float* w_oihw, void* packed, int32_t cout, int32_t ci
 
 int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s);
 /* Tuning entry point: same contract as isr_conv3x3_fwd with an explicit kernel
- * variant (0 = the production choice; others are tile / pipeline alternatives
- * kept for on-device A/B measurement).  Every variant of a default build writes
- * the same outputs as variant 0 (up to fp32 summation order); timing-only
- * ablations exist only in a library built with -DISR_TUNING.  Returns
- * ISR_ERR_UNSUPPORTED for an unknown variant. */
+ * variant (0 = the production choice).  The production library carries variant 0
+ * only; the tile / pipeline alternatives (1-3, 8, 9) and the timing-only ablations
+ * (4-7) exist in a library built with -DISR_TUNING (lib/libisr_tuning.so).  Every
+ * non-ablation variant writes the same outputs as variant 0 (up to fp32 summation
+ * order).  Returns ISR_ERR_UNSUPPORTED for a variant this library does not carry. */
 int isr_conv3x3_fwd_variant(const isr_conv_desc* d, int32_t variant, isr_stream_t s);
 /* Tuning builds (-DISR_TUNING) only: per-block wall-clock stamps of later conv3x3
  * launches into `buf` (8 x uint64 per block: entry, first chunk landed, main loop
@@ -405,7 +405,9 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
  * pair tile and ring with two 8-wave workgroups per CU (2 rows per wave, 4 waves per SIMD at
  * 128 VGPRs: one fragment set read a kernel row ahead, half the refill pieces per wave); 6 = the
  * production form with an XCD-aware tile deal (each XCD streams a contiguous range of tiles); 7 / 8 =
- * the production form with non-temporal halo loads / output stores. */
+ * the production form with non-temporal halo loads / output stores.  The production library
+ * carries variant 0 only (every other variant measured slower); variants 1-8 are
+ * built into the tuning library (-DISR_TUNING) and return ISR_ERR_UNSUPPORTED here. */
 int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
 /* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
  * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,
@@ -431,7 +433,9 @@ int isr_tail9x9_fwd(const isr_tail_desc* d, isr_stream_t s);
  * 8-row tile per block (76 KB LDS, 2 blocks / CU), 2 = persistent (one block per CU, streamed
  * halo ring), 4 = row-streaming walk down a 32-column strip (4 waves, each T row computed
  * once), 5 = the same walk with 8 waves (two per SIMD), 6 = lane-streaming walk (one wave per
- * strip, running ky sums shifted one lane per row).  All bit-identical.
+ * strip, running ky sums shifted one lane per row).  All bit-identical.  The production
+ * library carries 0, 3 (the fallback for outputs past 2 GiB) and 5; 1, 2, 4 and 6 are in the
+ * tuning library (-DISR_TUNING) only (ISR_ERR_UNSUPPORTED here).
  * Same descriptor rules as isr_tail9x9_fwd. */
 int isr_tail9x9_fwd_variant(const isr_tail_desc* d, int32_t variant, isr_stream_t s);
 

@@ -79,3 +79,62 @@ def test_allreduce_mean_flat_bucket():
         torch.testing.assert_close(a, torch.full((3, 2), 1.5))
         torch.testing.assert_close(b, torch.arange(4.0) * 1.5)
         torch.testing.assert_close(c, torch.tensor([0.5]))
+
+
+def _guard_worker(rank, world, port, q):
+    """A trunk give-up on rank 1 only: the step guard every rank's optimiser reads must say
+    "skip" on both ranks, and the epoch-end check must raise on both (the gradients
+    are averaged before the guard is read, so a per-rank guard lets peers apply poisoned ones)."""
+    import types
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from image_super_resolution_amd.engine import ChainFailed
+        from image_super_resolution_amd.train_engine import enable_grad_allreduce, step_guard_ptr, verify_chains
+
+        state = torch.zeros(8, dtype=torch.int32)
+        if rank == 1:
+            state[2] = 1  # sticky give-up count 1, accepted count 0
+
+        def verify():
+            if int(state[2]) != int(state[3]):
+                state[3] = state[2]
+                raise ChainFailed("gave up")
+
+        chain = types.SimpleNamespace(state=state, guard_ptr=state.data_ptr() + 8, verify=verify)
+        gen = torch.nn.Linear(2, 2)
+        gen.__dict__["_isr_train_plan"] = types.SimpleNamespace(chain=chain)
+        enable_grad_allreduce(gen, True)
+        ptr = step_guard_ptr(gen)
+        g = gen.__dict__["_isr_train_plan"]._global_guard
+        assert ptr == g.data_ptr()
+        words = g.tolist()
+        raised = False
+        try:
+            verify_chains(gen)
+        except ChainFailed:
+            raised = True
+        # after the report, the accepted count caught up: the next step's guard lets updates run
+        ptr2 = step_guard_ptr(gen)
+        q.put((rank, words, raised, g.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_trunk_give_up_guard_is_global_under_data_parallel():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_guard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (w, raised, w2) for r, w, raised, w2 in (q.get(timeout=120) for _ in range(2))}
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        words, raised, after = res[r]
+        assert words[0] != words[1], f"rank {r}: the guard must skip the step (words {words})"
+        assert raised, f"rank {r}: the epoch-end check must raise on every rank"
+        assert after[0] == after[1], f"rank {r}: once reported, later steps update again ({after})"

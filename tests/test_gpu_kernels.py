@@ -168,44 +168,45 @@ def test_tail9x9(u8):
 
 @pytest.mark.parametrize("n,h,w", [(2, 40, 72), (5, 128, 160), (3, 96, 64), (2, 300, 96)])
 def test_tail9x9_persistent_vs_per_tile(n, h, w):
-    """Persistent tail variant (one block per CU; (5, 128, 160) has 400 tiles, so blocks
-    walk several) vs the production one-tile-per-block kernel, and run-to-run bit equality.
-    The 8-row (3) and row-streaming (4, 5, 6; segment heights 16 / 128 / 32 / 16 here) variants
-    compute the same sums in the same order: bit-identical to the 16-row kernel."""
+    """The production row-streaming tail (variant 5, 8 waves; segment heights 16 / 128 / 32 / 16
+    here) vs the 8-row per-tile kernel (variant 3, its large-image fallback): the same sums in the
+    same order, so bit-identical, and run-to-run bit equality.  With the tuning library
+    (ISR_LIB=.../libisr_tuning.so) also the A/B forms: the 16-row per-tile kernel (1), the
+    persistent kernel (2), the 4-wave walk (4) and the lane-streaming walk (6)."""
     import ctypes
+    import os
     from image_super_resolution_amd import ops, _lib
     lib = _lib.load()
+    tuning = "tuning" in os.environ.get("ISR_LIB", "")
     x = _mk(n, 64, h, w, 21) * 0.5
     W = _w(3, 64, 9, 22)
     b = torch.randn(3, device=DEV) * 0.1
     xb = ops.ActBuffer.from_nchw(x, pad=4)
     wp = ops.pack_tail9x9(W)
-    outs = {}
-    for dt in (torch.float32, torch.uint8):
-        for v in (1, 2, 2):
-            o = torch.empty(n, 3, h, w, device=DEV, dtype=dt)
-            d = ops.tail9x9_desc(xb, wp, b, o)
-            ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(d), v, ops._stream()), "tail variant")
-            torch.cuda.synchronize()
-            outs.setdefault((dt, v), []).append(o)
-        o8 = torch.empty(n, 3, h, w, device=DEV, dtype=dt)  # 8-row, two-blocks-per-CU variant: same sums
-        d8 = ops.tail9x9_desc(xb, wp, b, o8)
-        ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(d8), 3, ops._stream()), "tail variant 3")
+
+    def run(v, dt, fill=None):
+        o = torch.empty(n, 3, h, w, device=DEV, dtype=dt) if fill is None else \
+            torch.full((n, 3, h, w), fill, device=DEV, dtype=dt)
+        d = ops.tail9x9_desc(xb, wp, b, o)
+        ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(d), v, ops._stream()), f"tail variant {v}")
         torch.cuda.synchronize()
-        a, p0, p1 = outs[(dt, 1)][0], outs[(dt, 2)][0], outs[(dt, 2)][1]
-        assert torch.equal(o8, a)
-        for v in (4, 5, 6):  # row-streaming variants (4 and 8 waves, lane-streaming)
-            os_ = torch.full((n, 3, h, w), 7, device=DEV, dtype=dt)
-            ds = ops.tail9x9_desc(xb, wp, b, os_)
-            ops.check(lib.isr_tail9x9_fwd_variant(ctypes.byref(ds), v, ops._stream()), f"tail variant {v}")
-            torch.cuda.synchronize()
-            assert torch.equal(os_, a), v
-        assert torch.equal(p0, p1)
-        if dt == torch.float32:
-            assert (a - p0).abs().max().item() < 1e-5
-        else:
-            dd = (a.float() - p0.float()).abs()
-            assert dd.max().item() <= 1 and (dd > 0).float().mean().item() < 1e-3
+        return o
+
+    for dt in (torch.float32, torch.uint8):
+        a = run(3, dt)
+        p0, p1 = run(5, dt, fill=7), run(5, dt, fill=7)
+        assert torch.equal(p0, a) and torch.equal(p1, a)
+        assert torch.equal(run(0, dt, fill=7), a)  # variant 0 = the production choice
+        if tuning:
+            for v in (1, 4, 6):
+                assert torch.equal(run(v, dt, fill=7), a), v
+            q0, q1 = run(2, dt), run(2, dt)  # persistent: its own order, run-to-run equal
+            assert torch.equal(q0, q1)
+            if dt == torch.float32:
+                assert (a - q0).abs().max().item() < 1e-5
+            else:
+                dd = (a.float() - q0.float()).abs()
+                assert dd.max().item() <= 1 and (dd > 0).float().mean().item() < 1e-3
 
 
 def test_bad_descriptor_raises():

@@ -45,7 +45,8 @@ class _Batches:
     def __init__(self, opt, target, rank, world, device):
         self.synthetic = opt.synthetic or not opt.data
         if self.synthetic:
-            self.src = data.SyntheticSR(opt.batch_size, target, seed=opt.seed * 131 + rank, device=device)
+            self.src = data.SyntheticSR(opt.batch_size, target, seed=opt.seed * 131 + rank, device=device,
+                                        kind=opt.synthetic_kind)
             self.n = opt.steps or 100
         else:
             from torch.utils.data import DataLoader, DistributedSampler
@@ -286,6 +287,9 @@ def parse(argv=None):
     p.add_argument("--data", type=str, default="", help="image directory or JSON list (default: ./train_images.json "
                    "if present, else synthetic)")
     p.add_argument("--synthetic", action="store_true")
+    p.add_argument("--synthetic_kind", default="smooth", choices=("smooth", "natural", "leaves"),
+                   help="synthetic HR crops: smooth (bicubic noise), natural (1/f^1.4 Gaussian fields) or "
+                        "leaves (dead-leaves images with a 1/f texture)")
     p.add_argument("--dist_backend", default="nccl", help="process-group backend for WORLD_SIZE > 1 "
                    "(nccl = RCCL; gloo only to rehearse several ranks sharing one GPU)")
     p.add_argument("--steps", type=int, default=0, help="iterations per epoch (0 = one pass over the data)")
