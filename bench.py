@@ -102,6 +102,11 @@ def parse():
     return ap.parse_args()
 
 
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line stays the only stdout line)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def load_traffic(round_tag: str) -> dict:
     """{family: PMC HBM bytes per launch} from profiles/<round>_pmc_traffic.json."""
     p = ROOT / "profiles" / f"{round_tag}_pmc_traffic.json"
@@ -320,6 +325,7 @@ def main():
         elapsed = tt.item()
 
     ms = elapsed / args.steps * 1e3
+    log(f"inference: {ms:.3f} ms per step")
     out_timed = out.float().cpu()  # the last timed step's output (the parity leg compares it)
     plan.verify()  # a persistent-chain give-up in any timed step (sticky count) voids the run: raises
     hr_px = n * (hw * S) * (hw * S)
@@ -391,7 +397,10 @@ def main():
                       "frac": round(max(f_over_p, b_over_bw) / ms, 4),
                       "mfma_frac": round(f_over_p / ms, 4), "hbm_frac": round(b_over_bw / ms, 4)}
 
+    log("per-kernel roofline timings done")
     train = train_leg(args, dev, world, rank) if args.train_steps > 0 else None
+    if train is not None:
+        log(f"train leg: {train['ms_per_step']} ms per step")
 
     result = None
     if rank == 0:
@@ -408,6 +417,8 @@ def main():
                 t1 = time.perf_counter()
                 refs.append(ref_cpu.generator(sd_cpu, x_cpu[i:i + 1], num_blocks=args.blocks, scale=S))
                 ts.append(time.perf_counter() - t1)
+                if i % 4 == 3:
+                    log(f"cpu baseline: {i + 1}/{nt} tiles")
             t_tile = statistics.median(ts[1:])
             cpu = {"value": round((hw * S) ** 2 / t_tile / 1e6, 4), "unit": "MPix/s",
                    "cores": cores["use"], "kind": "port",

@@ -250,8 +250,8 @@ int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_
         return fail(ISR_ERR_BAD_DESC, "conv chain: null layers / kinds / state or nl not in [1, 1024]");
     if (c->n <= 0 || c->ha <= 0 || c->wa <= 0 || c->ha % 16 || c->wa % 32)
         return fail(ISR_ERR_BAD_DESC, "conv chain: bad grid n=%d ha=%d wa=%d", c->n, c->ha, c->wa);
-    if (variant == 0 || (variant >= 2 && variant <= 8)) {
-        static const int form_of[9] = {0, 0, 1, 2, 3, 4, 5, 6, 7};
+    if (variant == 0 || (variant >= 2 && variant <= 9)) {
+        static const int form_of[10] = {0, 0, 1, 2, 3, 4, 5, 6, 7, 8};
         const int rc = isr::trunk_launch(c, (hipStream_t)s, form_of[variant]);
         if (rc == -3) return fail(ISR_ERR_UNSUPPORTED, "conv chain: variant %d is an A/B form of the tuning library "
                                   "(lib/libisr_tuning.so)", variant);

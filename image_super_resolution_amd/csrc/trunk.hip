@@ -36,7 +36,8 @@ size_t trunk_state_words(int n, int ha, int wa) {
 
 // ---- prep: validate the layer table and compile it into records; bump the generation ----
 // err bits: 1 grid, 2 view geometry, 4 kind/cout, 8 cin/bias, 16 unsupported epilogue form,
-// 32 residual form, 64 beyond the 2 GiB buffer window, 128 too many layers.
+// 32 residual form, 64 a 16-channel plane of 2 GiB or more (one buffer resource spans one plane),
+// 128 too many layers.
 __global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* layers, const int32_t* kinds, int nl,
                                                           int n, int ha, int wa, unsigned* state, int th) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -114,8 +115,8 @@ __global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* l
     }
     __syncthreads();
     if (L == 0) {
-        const size_t bytes = (size_t)n * (g0.x.cs / 16) * g0.x.hp * g0.x.wp * 32;
-        const unsigned e = *err | (bytes >= 0x7fffffffull ? 64u : 0u) | (nl > 1024 ? 128u : 0u);
+        const size_t plane = (size_t)g0.x.hp * g0.x.wp * 32;  // every buffer resource spans one plane
+        const unsigned e = *err | (plane >= 0x7fffffffull ? 64u : 0u) | (nl > 1024 ? 128u : 0u);
         uint32_t* geo = state + ro - 16;
         const int32_t gv[16] = {n, g0.h, g0.w, ha, wa, g0.x.hp, g0.x.wp, g0.x.cs / 16, g0.x.pad, nbx, nby, ntiles,
                                 (int32_t)e, 0, 0, 0};
@@ -229,12 +230,12 @@ struct TK {
 // Where the chunks of one (layer, tile) item come from (LDS-DMA through buffer resources:
 // 32-bit offsets, no per-piece 64-bit address arithmetic).
 struct Src {
-    const char* x;   // activation buffer base
-    uint32_t h0;     // byte offset of the halo origin of chunk 0: pixel (y0-1, x0-1) of plane xp
+    const char* x;   // base of the 16-channel plane chunk 0 reads (image img, plane xp)
+    uint32_t h0;     // in-plane byte offset of the halo origin: pixel (y0-1, x0-1)
     const char* w;   // packed weights of chunk 0
     const float* b;  // bias
     int wpc;         // weight pieces per chunk (9 / 18)
-    uint32_t xbytes, wbytes;  // extents of the activation buffer and of the packed weights
+    uint32_t xbytes, wbytes;  // extents of one activation plane and of the packed weights
 };
 
 template <class K>
@@ -244,8 +245,9 @@ struct TrunkCtx {
     unsigned gen;
     int acquire;
     int hp, wp, cs16, pad, h, w, nbx, nby, ntiles;
-    uint32_t pstride;            // bytes per 16-channel plane
-    uint32_t abytes;             // bytes of one activation buffer (< 2 GiB: prep err bit 64)
+    uint32_t pstride;            // bytes per 16-channel plane (< 2 GiB: prep err bit 64); every buffer
+                                 // resource spans ONE plane (a per-(image, plane) base), so the
+                                 // buffers themselves may be any size (the 4K still, video batches)
     uint32_t hoff[K::HPW];       // per-lane halo piece offsets (chunk-invariant)
     int abl;                     // tuning ablation bits (0 in production builds)
 };
@@ -254,13 +256,12 @@ template <class C>
 __device__ __forceinline__ Src src_of(const C& c, const_rec& rec, int t) {
     const int bx = t % c.nbx, tmp = t / c.nbx, by = tmp % c.nby, img = tmp / c.nby;
     Src s;
-    s.x = (const char*)(uintptr_t)rec.x;
-    s.h0 = (uint32_t)(((((uint32_t)img * c.cs16 + rec_xp(rec)) * c.hp + (by * C::TH - 1 + c.pad)) * c.wp +
-                       (bx * tk::TW - 1 + c.pad)) * 32);
+    s.x = (const char*)(uintptr_t)rec.x + (size_t)((uint32_t)img * c.cs16 + rec_xp(rec)) * c.pstride;
+    s.h0 = (uint32_t)(((by * C::TH - 1 + c.pad) * c.wp + (bx * tk::TW - 1 + c.pad)) * 32);
     s.w = (const char*)(uintptr_t)rec.w;
     s.b = (const float*)(uintptr_t)rec.b;
     s.wpc = rec_kind(rec) == 1 ? tk::WPF : tk::WPG;  // 64 / 32 couts (kinds 0 and 2: 32)
-    s.xbytes = c.abytes;
+    s.xbytes = c.pstride;
     s.wbytes = (uint32_t)(rec_nch(rec) * s.wpc * 1024);
     return s;
 }
@@ -276,8 +277,8 @@ __device__ __forceinline__ uint32_t stage_chunk_k(const uint32_t* hoff, uint32_t
     const int wave = wave_id(), lane = threadIdx.x & 63;
     char* dst = smem + slot * SLOTB;
     uint32_t n = 0;
-    const auto rx = rsrc_n(s.x, s.xbytes);
-    const uint32_t so = s.h0 + (uint32_t)chunk * pstride;
+    const auto rx = rsrc_n(s.x + (size_t)chunk * pstride, s.xbytes);  // chunk c = plane xp + c
+    const uint32_t so = s.h0;
     if (!(abl & 1)) {
 #pragma unroll
         for (int k = 0; k < HPW; ++k) {
@@ -383,7 +384,8 @@ constexpr int kTrunkInterleaveStep = ISR_TRUNK_INTERLEAVE == 2 ? 2 : 0;
 struct Refill {
     bool on;
     Src src;
-    uint32_t so, wo;   // halo source offset of the chunk, weight offset
+    const char* xb;    // the chunk's plane base
+    uint32_t so, wo;   // in-plane halo offset of the chunk, weight offset
     char* dst;         // slot base in LDS
     bool bias;
     int bslot;
@@ -398,7 +400,7 @@ __device__ __forceinline__ uint32_t refill_piece_k(const uint32_t* hoff, int abl
     if (p < HPW) {
         const int j = wave + WM * p;
         if (!(abl & 1) && j < HP) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(rf.src.x, rf.src.xbytes), ISR_LDS_PTR(rf.dst + j * 1024), 16, hoff[p],
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_n(rf.xb, rf.src.xbytes), ISR_LDS_PTR(rf.dst + j * 1024), 16, hoff[p],
                                                      rf.so, 0, 16);
             return 1;
         }
@@ -434,7 +436,8 @@ __device__ __forceinline__ Refill make_refill(const TrunkCtx<K>& c, const Src& s
     Refill rf;
     rf.on = true;
     rf.src = s;
-    rf.so = s.h0 + (uint32_t)chunk * c.pstride;
+    rf.xb = s.x + (size_t)chunk * c.pstride;
+    rf.so = s.h0;
     rf.wo = (uint32_t)(chunk * s.wpc * 1024);
     rf.dst = smem + slot * K::SLOT;
     rf.bias = with_bias;
@@ -784,28 +787,26 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     {
         typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
         const int xx = x0 + l31;
-        const auto yr = rsrc_n((const void*)(uintptr_t)rec.y, c.abytes);
         const float slope = rec.slope, s1 = rec.s1, s2 = rec.s2;
         const bool scale2 = s2 != 1.f;
-        const uint32_t plane_px = (uint32_t)(c.hp * c.wp);
-        const uint32_t ypl = (uint32_t)(img * c.cs16 + rec_yp(rec)) * plane_px;
+        // one buffer resource per output plane (cout channels = NF * 2 planes of 16): couts
+        // [32 f + 16 blk, + 16) live in plane yp + 2 f + blk of image img
+        const char* ybase = (const char*)(uintptr_t)rec.y + (size_t)((uint32_t)img * c.cs16 + rec_yp(rec)) * c.pstride;
         // RRDB residual (every third RDB's final conv): row r + 1's values are loaded while row r
         // is finished, so at most two rows (32 VGPRs) are live — loading them all before the last
         // chunk's MFMAs (64 VGPRs beside the 128 accumulators and the fragments) spilled.
         // Compiler-visible loads: hipcc places the wait before their first use itself.
         bf16x8 q2[R][NF][2];
-        const uint32_t r2pl = (uint32_t)(img * c.cs16 + rec_r2p(rec)) * plane_px;
-        const auto rr = rsrc_n((const void*)(uintptr_t)rec.r2, c.abytes);
+        const char* r2base = (const char*)(uintptr_t)rec.r2 + (size_t)((uint32_t)img * c.cs16 + rec_r2p(rec)) * c.pstride;
         auto load_r2 = [&](int r) {
             const uint32_t pix = (uint32_t)((y0 + wave * R + r + c.pad) * c.wp + xx + c.pad);
 #pragma unroll
             for (int f = 0; f < NF; ++f)
 #pragma unroll
                 for (int blk = 0; blk < 2; ++blk) {
-                    const int co = f * 32 + 16 * blk + 8 * hh;
+                    const auto rr = rsrc_n(r2base + (size_t)(2 * f + blk) * c.pstride, c.pstride);
                     q2[r][f][blk] = __builtin_bit_cast(
-                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                    rr, (r2pl + (uint32_t)(co >> 4) * plane_px + pix) * 32 + 16 * hh, 0, 16));
+                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, pix * 32 + 16 * hh, 0, 16));
                 }
             st.issued += NF * 2;
         };
@@ -843,8 +844,8 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                         }
                         if (!valid) u[e] = 0.f;
                     }
-                    const int co = f * 32 + 16 * blk + 8 * hh;
-                    const uint32_t off = (ypl + (uint32_t)(co >> 4) * plane_px + pix) * 32 + 16 * hh;
+                    const auto yr = rsrc_n(ybase + (size_t)(2 * f + blk) * c.pstride, c.pstride);
+                    const uint32_t off = pix * 32 + 16 * hh;
                     bf16x8 tq;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) tq[e] = (__bf16)u[e];
@@ -888,7 +889,6 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
     c.nby = g.nby;
     c.ntiles = g.ntiles;
     c.pstride = (uint32_t)(c.hp * c.wp * 32);
-    c.abytes = (uint32_t)((size_t)g.n * g.cs16 * c.pstride);
     c.abl = trunk_abl_load();
     {
         const int wave = wave_id(), lane = threadIdx.x & 63;
@@ -1017,8 +1017,11 @@ int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_deep.h
 int trunk_deep_knobs_set(const int* k);
 #endif
 
+int trunk_lc_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_lc.hip (loader / consumer form)
+
 int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
     if (form == 0) return trunk_launch_k<TK_PAIR>(cd, s);
+    if (form == 8) return trunk_lc_launch(cd, s);
 #ifdef ISR_TUNING
     if (form == 3) return trunk_deep_launch(cd, s);
     if (form == 2) return trunk_launch_k<TK_T32>(cd, s);

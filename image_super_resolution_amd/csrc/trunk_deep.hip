@@ -739,6 +739,8 @@ __global__ __launch_bounds__(td::NT, 2) void trunk_deep_kernel(unsigned* state, 
         shape_ok = shape_ok && (n % 2 == 0) && n >= 2 && rec_kind(c.recs[L]) != 2 &&
                    (rec_kind(c.recs[L]) == 0 || (rec_fold(c.recs[L]) && n >= 6));  // no masked (kind 2) layers
     }
+    // this A/B form addresses a whole activation buffer with 32-bit offsets: < 2 GiB only
+    if ((size_t)g.n * g.cs16 * g.hp * g.wp * 32 >= 0x7fffffffull) shape_ok = false;
     if (!shape_ok) {
         if (threadIdx.x == 0 && blockIdx.x == 0) {
             __hip_atomic_store(state + 1, c.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

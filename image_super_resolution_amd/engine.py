@@ -291,8 +291,9 @@ class ConvChain:
                                  "1/s1 exact in bf16)")
             if d.r2.data and not d.r1.data:
                 raise ValueError("conv chain: r2 without r1")
-        if grid.t.numel() * 2 >= 2 ** 31:
-            raise ValueError("conv chain: activation buffers must stay below 2 GiB (buffer-descriptor window)")
+        if grid.t.shape[2] * grid.t.shape[3] * 32 >= 2 ** 31:  # the trunk kernel's buffer resources span one 16-channel plane
+            raise ValueError("conv chain: a 16-channel activation plane must stay below 2 GiB (buffer-descriptor "
+                             "window)")
         self.variant = CHAIN_VARIANT if variant is None else variant
         if self.variant in (3, 4) and grid.ha % 32:
             raise ValueError(f"conv chain: variant {self.variant} (32x32 trunk tiles) needs the padded height "

@@ -93,8 +93,8 @@ def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | N
     splits into `world` x k full-width bands of equal core height (the last one ragged), each
     extended by `halo` LR rows above and below (clipped to the image, like a window's halo);
     rank r takes the k contiguous bands [r k, (r + 1) k).  k is the smallest count that keeps a
-    band's input within `max_rows` (the persistent trunk kernel's 2 GiB buffer window by
-    default, see band_max_rows).  EVERY band has the same input height, min(height, core +
+    band's input within `max_rows` (the persistent trunk kernel's 2 GiB window per 16-channel
+    plane by default, see band_max_rows).  EVERY band has the same input height, min(height, core +
     2 halo): an image-edge band (halo clipped at the edge) or the ragged last band extends its
     input further into the image instead (more context than the halo asks, never less), so a
     rank builds ONE plan for all its bands and runs each as one batch-1 forward over the full
@@ -128,8 +128,8 @@ def plan_blocks(height: int, width: int, world: int, halo: int, limit: int = 2 *
     blocks of equal core (split evenly: cores differ by at most one pixel), each extended by `halo` LR pixels on every
     side and clipped at the image edge (a true image edge is the network's own zero padding, so
     clipping loses no context the whole-image forward has); rank r takes blocks [r k, (r + 1) k)
-    in raster order.  k is the smallest count whose blocks fit the trunk kernel's 2 GiB buffer
-    window; among the grids of that count the one with the least work on the busiest rank wins
+    in raster order.  k is the smallest count whose blocks fit the trunk kernel's 2 GiB window per
+    16-channel plane (any still up to ~8K x 8K LR fits whole: k = 1); among the grids of that count the one with the least work on the busiest rank wins
     (work = the blocks' tile-aligned LR area, what the trunk kernel computes).  Full-width bands
     are the gc = 1 member of this family; at cfg4 over 8 ranks the 2 x 4 grid puts 1.14 M LR px
     on the busiest rank against 1.29 M for the 334-row bands (halo 32: 8 % vs 24 % overhead).
@@ -151,7 +151,7 @@ def plan_blocks(height: int, width: int, world: int, halo: int, limit: int = 2 *
 
     def fits(t: Tile) -> bool:
         h, w = t.in_shape
-        return 192 * 2 * (round_up(h, TILE_H) + 2) * (round_up(w, TILE_W) + 2) < limit
+        return 16 * 2 * (round_up(h, TILE_H) + 2) * (round_up(w, TILE_W) + 2) < limit
 
     k = 1
     while True:
@@ -179,11 +179,12 @@ def plan_blocks(height: int, width: int, world: int, halo: int, limit: int = 2 *
 
 
 def band_max_rows(width: int, limit: int = 2 ** 31) -> int:
-    """Largest band input height whose 192-channel dense buffer (engine.GeneratorBuffers:
-    bf16, 16x32-rounded, 1-px border) stays below the trunk kernel's 2 GiB buffer window."""
+    """Largest band input height whose 16-channel activation plane (engine.GeneratorBuffers:
+    bf16, 16x32-rounded, 1-px border) stays below the trunk kernel's 2 GiB window (its buffer
+    resources span one plane each)."""
     from .ops import TILE_H, TILE_W, round_up
     wa = round_up(width, TILE_W) + 2
-    rows = limit // (192 * 2 * wa) - 2
+    rows = limit // (16 * 2 * wa) - 2
     return max(TILE_H, rows // TILE_H * TILE_H - TILE_H)
 
 
@@ -278,9 +279,9 @@ class TileUpscaler:
         """`shard`: "windows" runs rs.py's windows (dealt longest-processing-time-first over
         ranks, shard_tiles; the canvas equals the single-rank one bit for bit); "bands" runs
         full-width horizontal bands with the same halo (plan_bands: one rank's share is one or a
-        few bands of one input shape, one batch-1 forward each — `batch` applies to windows only;
-        on one GPU the image splits into as few bands as the trunk kernel's 2 GiB buffer window
-        allows; needs halo > 0 to hide its seams, and differs from the windowed canvas by the
+        few bands of one input shape, `batch` bands per forward; on one GPU the image splits into
+        as few bands as the trunk kernel's 2 GiB window per activation plane allows (one, up to
+        ~8K x 8K LR); needs halo > 0 to hide its seams, and differs from the windowed canvas by the
         seams each form leaves); "blocks" runs a 2-D grid of blocks with the same halo (plan_blocks:
         at cfg4 over 8 ranks 2 x 4 blocks, 8 % halo work instead of the bands' 24 %).
         `gather` (world > 1): "device" sends every finished tile to rank 0's device canvas point to
@@ -296,9 +297,6 @@ class TileUpscaler:
             raise ValueError(f"gather must be 'device' or 'host', got {gather!r}")
         if shard != "windows" and halo == 0:
             warnings.warn(f"shard={shard!r} with halo=0: the seams are not hidden (pass halo > 0)", stacklevel=2)
-        if shard != "windows" and batch != 1:
-            warnings.warn(f"shard={shard!r} runs every band / block as one batch-1 forward; batch={batch} is "
-                          "ignored", stacklevel=2)
         self.runner, self.scale, self.window, self.halo, self.batch = runner, scale, window, halo, batch
         self.device = torch.device(device)
         self.shard = shard
@@ -321,8 +319,7 @@ class TileUpscaler:
         for t in tiles:
             groups[t.in_shape].append(t)
         out: dict[int, torch.Tensor] = {}
-        # bands are sized to the trunk kernel's 2 GiB buffer window one at a time: batch 1
-        step = 1 if self.shard != "windows" else self.batch
+        step = self.batch  # windows, bands and blocks of one input shape share a batched forward
         for (h, w), lst in groups.items():
             for i in range(0, len(lst), step):
                 chunk = lst[i:i + step]

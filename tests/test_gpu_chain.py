@@ -14,7 +14,8 @@ from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-# The production libisr.so carries the production trunk form (variant 0) only; the A/B forms are
+# The production libisr.so carries the production trunk forms (variant 0, the pair form, and 9, the
+# loader / consumer form of trunk_lc.hip); the A/B forms are
 # built into lib/libisr_tuning.so (ISR_LIB=.../libisr_tuning.so runs this file on all of them).
 TUNING_LIB = "tuning" in os.environ.get("ISR_LIB", "")
 
@@ -62,14 +63,18 @@ def _inputs(n, h, w, k, seed):
 # (4, 512, 512) = 2,048 tiles and (1, 540, 960) = 1,020 ragged tiles: more tiles than the 512
 # resident workgroups of a 256-CU chip, so every workgroup walks several tiles per layer (the
 # video and 4K-still geometry)
+# (10, 768, 768): every dense buffer is 2.28 GB, past the 2 GiB a single buffer resource can span —
+# the trunk kernel addresses each 16-channel plane through its own resource (round 5)
 @pytest.mark.parametrize("n,h,w,blocks", [(2, 36, 52, 2), (1, 128, 128, 1), (16, 128, 128, 16), (4, 256, 256, 2),
-                                          (4, 512, 512, 1), (1, 540, 960, 1)])
+                                          (4, 512, 512, 1), (1, 540, 960, 1), (10, 768, 768, 1)])
 def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks):
     gw = _gw(blocks)
     xs = _inputs(n, h, w, 3, seed=3)
     refs = _run(gw, xs, chain=False)
     # variants 3 and 4 (32x32 tiles) need the 16-row-rounded height to be a multiple of 32
-    variants = ((0, 7, 8, 6, 5, 2, 1) + ((3, 4) if -(-h // 16) % 2 == 0 else ())) if TUNING_LIB else (0,)
+    variants = ((0, 9, 7, 8, 6, 5, 2, 1) + ((3, 4) if -(-h // 16) % 2 == 0 else ())) if TUNING_LIB else (0,)
+    if os.environ.get("ISR_TEST_CHAIN_VARIANTS"):
+        variants = tuple(int(v) for v in os.environ["ISR_TEST_CHAIN_VARIANTS"].split(","))
     for variant in variants:
         for acquire in (False, True):
             for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire, variant=variant), refs):
