@@ -1017,12 +1017,14 @@ int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_deep.h
 int trunk_deep_knobs_set(const int* k);
 #endif
 
+#ifdef ISR_TUNING
 int trunk_lc_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_lc.hip (loader / consumer form)
+#endif
 
 int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
     if (form == 0) return trunk_launch_k<TK_PAIR>(cd, s);
-    if (form == 8) return trunk_lc_launch(cd, s);
 #ifdef ISR_TUNING
+    if (form == 8) return trunk_lc_launch(cd, s);
     if (form == 3) return trunk_deep_launch(cd, s);
     if (form == 2) return trunk_launch_k<TK_T32>(cd, s);
     if (form == 4) return trunk_launch_k<TK_QUAD>(cd, s);
@@ -1035,8 +1037,10 @@ int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
 }
 
 #ifdef ISR_TUNING
+int trunk_lc_knobs_set(const int* k);  // trunk_lc.hip
 int trunk_knobs_set(const int* k) {
     g_trunk_per_cu = k[1];
+    if (trunk_lc_knobs_set(k) != 0) return -1;
     if (trunk_deep_knobs_set(k) != 0) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
 }

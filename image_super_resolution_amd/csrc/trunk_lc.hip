@@ -28,6 +28,10 @@
 
 namespace isr {
 
+// An A/B form: bitwise equal to the per-conv launches, but 1-3 % SLOWER than the pair form on the
+// bench forward — compiled into the tuning library only.
+#ifdef ISR_TUNING
+
 namespace lc {
 constexpr int WMC = 4;                          // compute waves
 constexpr int WML = 4;                          // loader waves
@@ -47,6 +51,19 @@ static_assert(LDS <= 163840, "LDS budget");
 static_assert(INFL < NS, "a loader never waits for a slot whose chunk it has not handed over");
 }  // namespace lc
 
+// Tuning builds: ablation bits (timing only, outputs wrong): 1 = loaders skip the halo DMA, 8 = the
+// weight DMA, 16 = the dependency waits; 2 = compute waves skip fragment reads and MFMAs, 4 = the
+// epilogue stores.
+#ifdef ISR_TUNING
+__device__ int g_lc_knobs[4];
+__device__ __forceinline__ int lc_abl_load() { return __builtin_amdgcn_readfirstlane(g_lc_knobs[0]); }
+int trunk_lc_knobs_set(const int* k) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_lc_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
+}
+#else
+__device__ __forceinline__ int lc_abl_load() { return 0; }
+#endif
+
 struct LcArgs {
     unsigned* state;
     int rec_off;   // words
@@ -60,6 +77,7 @@ struct LcCtx {
     int acquire;
     int hp, wp, cs16, pad, h, w, nbx, nby, ntiles;
     uint32_t pstride;  // bytes per 16-channel plane (< 2 GiB): each buffer resource spans one
+    int abl;           // tuning ablation bits (0 in production builds)
 };
 
 // ---- LDS words (flags) -------------------------------------------------------------------
@@ -141,7 +159,9 @@ __device__ __forceinline__ void lc_hand_all(LcPend& p) {
     p.n = 0;
 }
 
-__device__ void lc_loader(const LcCtx& c, const_rec* recs, int nl, int G, int b, int lw) {
+// forceinline: as an outlined call its context went through scratch, and scratch loads counted in
+// vmcnt would weaken the counted waits that hand chunks to the consumers
+__device__ __forceinline__ void lc_loader(const LcCtx& c, const_rec* recs, int nl, int G, int b, int lw) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     uint32_t hoff[lc::HPW];
@@ -173,7 +193,7 @@ __device__ void lc_loader(const LcCtx& c, const_rec* recs, int nl, int G, int b,
                     const unsigned tgt = 4u * (item / lc::NS);
                     if ((int)(lds_word(lc_free(slot)) - tgt) < 0) lds_wait_ge(c, lc_free(slot), tgt);
                 }
-                if (!dep_ok && ch >= first_new) {
+                if (!dep_ok && ch >= first_new && !(c.abl & 16)) {
                     // every landed chunk goes to the consumers first: the neighbourhood may be
                     // waiting for this workgroup's own tiles
                     lc_hand_all(p);
@@ -186,7 +206,7 @@ __device__ void lc_loader(const LcCtx& c, const_rec* recs, int nl, int G, int b,
 #pragma unroll
                 for (int k = 0; k < lc::HPW; ++k) {
                     const int j = lw + lc::WML * k;
-                    if (j < lc::HP) {
+                    if (j < lc::HP && !(c.abl & 1)) {
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, ISR_LDS_PTR(dst + j * 1024), 16, hoff[k], h0, 0, 16);
                         ++issued;
                     }
@@ -195,7 +215,7 @@ __device__ void lc_loader(const LcCtx& c, const_rec* recs, int nl, int G, int b,
 #pragma unroll
                 for (int k = 0; k < lc::WPW; ++k) {
                     const int j = lw + lc::WML * k;
-                    if (j < wpc) {
+                    if (j < wpc && !(c.abl & 8)) {
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, ISR_LDS_PTR(dst + (lc::HP + j) * 1024), 16,
                                                                  lane * 16, wo + j * 1024, 0, 0);
                         ++issued;
@@ -221,9 +241,25 @@ __device__ void lc_loader(const LcCtx& c, const_rec* recs, int nl, int G, int b,
 }
 
 // ---- compute waves -------------------------------------------------------------------------
+// A finished tile whose progress word is not yet published (its stores are drained later, behind
+// the next tile's first chunk, instead of stalling the matrix pipe right after the epilogue).
+struct LcPub {
+    bool pend;
+    int t, tseq;
+    unsigned v;
+};
+
+__device__ __forceinline__ void lc_publish(const LcCtx& c, LcPub& pb) {
+    if (!pb.pend) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
+    if (lds_inc_rtn(LC_DONE) == 4u * (unsigned)pb.tseq + 3u && (threadIdx.x & 63) == 0)  // the last wave
+        __hip_atomic_store(c.state + 4 + pb.t, pb.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pb.pend = false;
+}
+
 template <int NF, bool MASKED>
-__device__ __forceinline__ void lc_tile(const LcCtx& c, unsigned& item, int tseq, const_rec& rec, int L, int t,
-                                        int wave) {
+__device__ __forceinline__ void lc_tile(const LcCtx& c, unsigned& item, LcPub& pb, int tseq, const_rec& rec, int L,
+                                        int t, int wave) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int R = lc::R, TN = lc::TN, NA = lc::NA, CT = 32 * NF;
     const int lane = threadIdx.x & 63, l31 = lane & 31, hh = lane >> 5;
@@ -241,60 +277,95 @@ __device__ __forceinline__ void lc_tile(const LcCtx& c, unsigned& item, int tseq
         a_h[dx] = (uint32_t)((wave * R * tk::HC + l31 + dx) * 32 + 16 * (hh ^ (((l31 + dx) >> 3) & 1)));
     const uint32_t idv = rec_idv(rec);
     f32x16 acc[R][NF];
-
-    auto do_chunk = [&](const int ch, auto fc_tag) {
-        constexpr int FC = decltype(fc_tag)::value;
-        const int slot = (int)(item % lc::NS);
-        lds_wait_ge(c, lc_full(slot), 4u * (item / lc::NS + 1));
-        if (ch == 0) {  // bias -> accumulators (register g of lane l: cout (g&3) + 8(g>>2) + 4hh)
-            const float* bs = reinterpret_cast<const float*>(smem + lc::BIAS_OFF + bslot * 256);
-#pragma unroll
-            for (int f = 0; f < NF; ++f) {
-                f32x16 b0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const f32x4 q = *reinterpret_cast<const f32x4*>(bs + f * 32 + 8 * j + 4 * hh);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) b0[4 * j + e] = q[e];
-                }
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r][f] = b0;
-            }
+    // two fragment sets: chunk ch computes step s from set (s + ch) & 1, so during its step 2 the
+    // other set is free for the NEXT chunk's step-0 fragments (read there when that chunk's slot
+    // is already full: no exposed read latency and no FULL wait at the next chunk's top)
+    bf16x8 fb[2][TN][NF], fa[2][NA];
+    auto read_one = [&](const char* sb, int dx, int idx, int set) {
+        if (idx < TN * NF) {
+            const int dyi = idx / NF, f = idx % NF;
+            fb[set][dyi][f] = lds_read16(sb + a_w + ((dyi * 3 + dx) * CT * 2 + f * 64) * 16);
+        } else {
+            const int ia = idx - TN * NF;
+            fa[set][ia] = lds_read16(sb + a_h[dx] + ia * tk::HC * 32);
         }
+    };
+    // step 0's q-th fragment in order of first use (kernel-row-major MFMA order): kernel row 0's
+    // weights, input rows 0..R-1, kernel row 1's weights, row R, kernel row 2's weights, row R+1
+    constexpr int NS0 = TN * NF + NA;
+    auto read_s0 = [&](const char* sb, int q, int set) {
+        if (q < NF) read_one(sb, 0, q, set);
+        else if (q < NF + R) read_one(sb, 0, TN * NF + (q - NF), set);
+        else if (q < 2 * NF + R) read_one(sb, 0, NF + (q - NF - R), set);
+        else if (q == 2 * NF + R) read_one(sb, 0, TN * NF + R, set);
+        else if (q < 3 * NF + R + 1) read_one(sb, 0, 2 * NF + (q - 2 * NF - R - 1), set);
+        else read_one(sb, 0, TN * NF + R + 1, set);
+    };
+    bool pf = false;  // the current chunk's step-0 fragments were read by the previous chunk
+    // the previous tile's publish, as plain locals: a struct reference live across the inline-asm
+    // waits here was kept in memory by hipcc (scratch spills around every chunk)
+    bool ppend = pb.pend;
+    const int pt = pb.t, ptseq = pb.tseq;
+    const unsigned pv = pb.v;
+    auto publish_prev = [&]() {
+        if (!ppend) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lds_inc_rtn(LC_DONE) == 4u * (unsigned)ptseq + 3u && (threadIdx.x & 63) == 0)
+            __hip_atomic_store(c.state + 4 + pt, pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ppend = false;
+    };
+
+    auto do_chunk = [&](const int ch, auto fc_tag, auto p_tag) {
+        constexpr int FC = decltype(fc_tag)::value, P = decltype(p_tag)::value;
+        const int slot = (int)(item % lc::NS);
         const char* sb = smem + slot * lc::SLOT;
-        bf16x8 fb[2][TN][NF], fa[2][NA];
-        auto read_one = [&](int dx, int idx, int set) {
-            if (idx < TN * NF) {
-                const int dyi = idx / NF, f = idx % NF;
-                fb[set][dyi][f] = lds_read16(sb + a_w + ((dyi * 3 + dx) * CT * 2 + f * 64) * 16);
-            } else {
-                const int ia = idx - TN * NF;
-                fa[set][ia] = lds_read16(sb + a_h[dx] + ia * tk::HC * 32);
+        if (!pf) {
+            const unsigned tgt = 4u * (item / lc::NS + 1);
+            if (ppend && (int)(lds_word(lc_full(slot)) - tgt) < 0) publish_prev();  // never wait holding it
+            lds_wait_ge(c, lc_full(slot), tgt);
+            if (ch == 0) {  // bias -> accumulators (register g of lane l: cout (g&3) + 8(g>>2) + 4hh)
+                const float* bs = reinterpret_cast<const float*>(smem + lc::BIAS_OFF + bslot * 256);
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    f32x16 b0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const f32x4 q = *reinterpret_cast<const f32x4*>(bs + f * 32 + 8 * j + 4 * hh);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) b0[4 * j + e] = q[e];
+                    }
+#pragma unroll
+                    for (int r = 0; r < R; ++r) acc[r][f] = b0;
+                }
             }
-        };
-        auto read_fb = [&](int dx, int dyi, int set) {
+            if (c.abl & 2) {  // tuning ablation: no fragment reads, no MFMAs
+                lds_inc(lc_free(slot));
+                ++item;
+                return;
+            }
 #pragma unroll
-            for (int f = 0; f < NF; ++f) read_one(dx, dyi * NF + f, set);
-        };
-        // step 0's fragments in order of first use (kernel-row-major MFMA order below)
-        read_fb(0, 0, 0);
-#pragma unroll
-        for (int ia = 0; ia < R; ++ia) read_one(0, TN * NF + ia, 0);
-        read_fb(0, 1, 0);
-        read_one(0, TN * NF + R, 0);
-        read_fb(0, 2, 0);
-        read_one(0, TN * NF + R + 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
+            for (int q = 0; q < NS0; ++q) read_s0(sb, q, P);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        pf = false;
         __builtin_amdgcn_s_setprio(1);
         // MFMAs: 3 steps (dx), each kernel-row-major (dy, then output row r) — every accumulator
         // sees dy 0, 1, 2 in that order, as in trunk.hip and conv3x3.hip (bit-identical sums)
 #pragma unroll
         for (int stp = 0; stp < 3; ++stp) {
-            const int cur = stp & 1;
+            const int cur = (stp + P) & 1;
+            bool pre = false;
+            const char* nsb = sb;
             if (stp == 2) {
                 // every LDS read of this slot has been issued (step 2's fragments were read during
                 // step 1): LDS executes a wave's ops in order, so the slot may be refilled now
                 lds_inc(lc_free(slot));
+                // the next slot's step-0 fragments are read below in any case (unconditional reads
+                // keep the free set's old values dead); they count only when that chunk belongs to
+                // this tile and its slot was already full here
+                const int nslot = (int)((item + 1) % lc::NS);
+                nsb = smem + nslot * lc::SLOT;
+                pre = ch + 1 < nch && (int)(lds_word(lc_full(nslot)) - 4u * ((item + 1) / lc::NS + 1)) >= 0;
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
@@ -309,29 +380,36 @@ __device__ __forceinline__ void lc_tile(const LcCtx& c, unsigned& item, int tseq
                             acc[r][FC >> 1] = mfma32(a, fa[cur][r + 1], acc[r][FC >> 1]);
                         }
                     }
-                    if (stp + 1 < 3 && (dyi == 2 || r == 0)) read_one(stp + 1, TN * NF + r + dyi, cur ^ 1);
+                    if (stp + 1 < 3 && (dyi == 2 || r == 0)) read_one(sb, stp + 1, TN * NF + r + dyi, cur ^ 1);
+                    if (stp == 2 && dyi * R + r < NS0) read_s0(nsb, dyi * R + r, cur ^ 1);
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 if (stp + 1 < 3) {
-                    read_fb(stp + 1, dyi, cur ^ 1);
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) read_one(sb, stp + 1, dyi * NF + f, cur ^ 1);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+            if (stp == 2) pf = pre;
         }
         __builtin_amdgcn_s_setprio(0);
         ++item;
+        publish_prev();  // the previous tile's stores are long done by now
     };
     int ch0 = 0;
     if constexpr (NF == 2) {
         if (fold && nch >= 4) {
-            do_chunk(0, TIC<0>{});
-            do_chunk(1, TIC<1>{});
-            do_chunk(2, TIC<2>{});
-            do_chunk(3, TIC<3>{});
+            do_chunk(0, TIC<0>{}, TIC<0>{});
+            do_chunk(1, TIC<1>{}, TIC<1>{});
+            do_chunk(2, TIC<2>{}, TIC<0>{});
+            do_chunk(3, TIC<3>{}, TIC<1>{});
             ch0 = 4;
         }
     }
-    for (int ch = ch0; ch < nch; ++ch) do_chunk(ch, TIC<-1>{});
+    for (int ch = ch0; ch < nch; ch += 2) {  // chunk parity = ch & 1 (compile-time set indices; nch even)
+        do_chunk(ch, TIC<-1>{}, TIC<0>{});
+        do_chunk(ch + 1, TIC<-1>{}, TIC<1>{});
+    }
 
     // ---- epilogue: straight from the accumulators, write-through (sc1) stores (trunk.hip) ----
     {
@@ -390,16 +468,18 @@ __device__ __forceinline__ void lc_tile(const LcCtx& c, unsigned& item, int tseq
                     bf16x8 tq;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) tq[e] = (__bf16)u[e];
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tq), yr, pix * 32 + 16 * hh, 0, 16);
+                    if (!(c.abl & 4))
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tq), yr, pix * 32 + 16 * hh, 0, 16);
                 }
             }
         }
     }
-    // publish: every compute wave drains its stores, the last one to arrive stores the progress word
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lds_inc_rtn(LC_DONE) == 4u * (unsigned)tseq + 3u && (threadIdx.x & 63) == 0)
-        __hip_atomic_store(c.state + 4 + t, c.gen * 1024u + (unsigned)(L + 1), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    publish_prev();
+    // published after the next tile's first chunk (or before any wait that could need it)
+    pb.pend = true;
+    pb.t = t;
+    pb.tseq = tseq;
+    pb.v = c.gen * 1024u + (unsigned)(L + 1);
 }
 
 // 512 threads, one workgroup per CU (2 waves per SIMD: up to 256 VGPRs)
@@ -428,6 +508,17 @@ __global__ __launch_bounds__(lc::NT, 1) void trunk_lc_kernel(LcArgs a) {
     c.nby = g.nby;
     c.ntiles = g.ntiles;
     c.pstride = (uint32_t)(c.hp * c.wp * 32);
+    c.abl = lc_abl_load();
+    // the compute waves walk a tile's chunks in pairs (alternating fragment sets): cin % 32 == 0
+    bool even = true;
+    for (int L = 0; L < a.nl; ++L) even = even && (rec_nch(recs[L]) % 2 == 0);
+    if (!even) {
+        if (threadIdx.x == 0 && blockIdx.x == 0) {
+            __hip_atomic_store(a.state + 1, c.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.state + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
     if (threadIdx.x < 16) reinterpret_cast<unsigned*>(smem + lc::FLAG_OFF)[threadIdx.x] = 0u;
     __syncthreads();
     const int G = gridDim.x, b = blockIdx.x, wave = wave_id();
@@ -438,15 +529,20 @@ __global__ __launch_bounds__(lc::NT, 1) void trunk_lc_kernel(LcArgs a) {
     }
     unsigned item = 0;
     int tseq = 0;
+    LcPub pb;
+    pb.pend = false;
+    pb.t = pb.tseq = 0;
+    pb.v = 0;
     for (int L = 0; L < a.nl; ++L) {
         const_rec& rec = recs[L];
         const int kind = rec_kind(rec);
         for (int t = b; t < c.ntiles; t += G, ++tseq) {
-            if (kind == 0) lc_tile<1, false>(c, item, tseq, rec, L, t, wave);
-            else if (kind == 2) lc_tile<1, true>(c, item, tseq, rec, L, t, wave);
-            else lc_tile<2, false>(c, item, tseq, rec, L, t, wave);
+            if (kind == 0) lc_tile<1, false>(c, item, pb, tseq, rec, L, t, wave);
+            else if (kind == 2) lc_tile<1, true>(c, item, pb, tseq, rec, L, t, wave);
+            else lc_tile<2, false>(c, item, pb, tseq, rec, L, t, wave);
         }
     }
+    lc_publish(c, pb);
 }
 
 // Grid: one workgroup per CU, every one resident (tiles wait on other workgroups' tiles).
@@ -480,5 +576,7 @@ int trunk_lc_launch(const isr_chain_desc* cd, hipStream_t s) {
     hipLaunchKernelGGL(trunk_lc_kernel, dim3(grid), dim3(lc::NT), lc::LDS, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+#endif  // ISR_TUNING
 
 }  // namespace isr

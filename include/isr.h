@@ -405,9 +405,12 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
  * pair tile and ring with two 8-wave workgroups per CU (2 rows per wave, 4 waves per SIMD at
  * 128 VGPRs: one fragment set read a kernel row ahead, half the refill pieces per wave); 6 = the
  * production form with an XCD-aware tile deal (each XCD streams a contiguous range of tiles); 7 / 8 =
- * the production form with non-temporal halo loads / output stores.  The production library
- * carries variant 0 only (every other variant measured slower); variants 1-8 are
- * built into the tuning library (-DISR_TUNING) and return ISR_ERR_UNSUPPORTED here. */
+ * the production form with non-temporal halo loads / output stores; 9 = trunk_lc.hip, the loader /
+ * consumer form: one 8-wave workgroup per CU, 4 compute waves on the pair form's tile and MFMA order,
+ * 4 loader waves filling a 4-slot LDS ring (FULL / FREE counts in LDS), the last compute wave of a
+ * tile publishing its progress word.  The production library carries variant 0 only (every other
+ * variant measured slower); variants 1-9 are built into the tuning library
+ * (-DISR_TUNING) and return ISR_ERR_UNSUPPORTED here. */
 int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
 /* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
  * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,

@@ -14,8 +14,8 @@ from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-# The production libisr.so carries the production trunk forms (variant 0, the pair form, and 9, the
-# loader / consumer form of trunk_lc.hip); the A/B forms are
+# The production libisr.so carries the production trunk form (variant 0) only; the A/B forms (9 = the
+# loader / consumer form of trunk_lc.hip, round 5) are
 # built into lib/libisr_tuning.so (ISR_LIB=.../libisr_tuning.so runs this file on all of them).
 TUNING_LIB = "tuning" in os.environ.get("ISR_LIB", "")
 

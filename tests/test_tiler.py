@@ -119,7 +119,8 @@ def test_bands_single_rank_equals_whole_image():
                                              (45, 61, 3, 1), (5, 9, 8, 1), (100, 7, 4, 0)])
 def test_plan_blocks_cover_and_halo(h, w, world, halo):
     """Blocks cover every LR pixel exactly once; each block's input is its core plus the halo on
-    every side, clipped to the image; every block fits the trunk kernel's buffer window."""
+    every side, clipped to the image; every block's 16-channel activation plane fits the trunk
+    kernel's 2 GiB buffer-resource window."""
     shards = tiler.plan_blocks(h, w, world, halo)
     assert len(shards) == world and all(len(s) == len(shards[0]) for s in shards)
     cover = torch.zeros(h, w, dtype=torch.int32)
@@ -128,7 +129,7 @@ def test_plan_blocks_cover_and_halo(h, w, world, halo):
         assert (b.y0, b.x0) == (max(0, b.y - halo), max(0, b.x - halo))
         assert (b.y1, b.x1) == (min(h, b.y + b.h + halo), min(w, b.x + b.w + halo))
         bh, bw = b.in_shape
-        assert 192 * 2 * (-(-bh // 16) * 16 + 2) * (-(-bw // 32) * 32 + 2) < 2 ** 31
+        assert 16 * 2 * (-(-bh // 16) * 16 + 2) * (-(-bw // 32) * 32 + 2) < 2 ** 31  # one 16-channel plane
     assert bool((cover == 1).all())
 
 

@@ -19,7 +19,7 @@ cp $T/prof_bench/bench_kernel_stats.csv $P/${R}_bench_kernel_stats.csv
 python3 - "$T/prof_bench/bench_kernel_trace.csv" "$P/${R}_bench_dominant_by_grid.json" <<'EOF2'
 import csv, json, sys
 from collections import defaultdict
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "trunk_kernel" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "trunk_" in r["Kernel_Name"] and "prep" not in r["Kernel_Name"]]
 by = defaultdict(list)
 for r in rows:
     by[int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
@@ -29,7 +29,7 @@ out = [{"kernel": rows[0]["Kernel_Name"], "blocks": b, "dispatches": len(v), "av
 json.dump(out, open(sys.argv[2], "w"), indent=1)
 print(json.dumps(out))
 EOF2
-bash tools/profile_pmc.sh $T/pmc_bench bench.py --no-cpu-baseline --steps 5 --warmup 2 --round $R
+bash tools/profile_pmc.sh $T/pmc_bench bench.py --no-cpu-baseline --steps 5 --warmup 2 --train-steps 0 --round $R
 python3 tools/pmc_summary.py $T/pmc_bench --json $P/${R}_pmc_summary.json > /dev/null
 python3 - "$R" "$P" <<'EOF'
 import json, sys
@@ -37,7 +37,7 @@ R, P = sys.argv[1], sys.argv[2]
 rows = json.load(open(f"{P}/{R}_pmc_summary.json"))
 # kernel families bench.py reports a roofline for (bench.py load_traffic): the persistent
 # trunk kernel, the per-conv growth (V_G0) and final (V_F0) templates, the 9x9 tail
-fam = {"chain": "trunk_kernel<", "growth": "C3<4, 4, 1, 16, 2, 0, 0, 2",
+fam = {"chain": "trunk_", "growth": "C3<4, 4, 1, 16, 2, 0, 0, 2",
        "final": "C3<4, 4, 2, 16, 2, 192", "tail": "tail9x9_"}
 out = {"families": {},
        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, KiB -> bytes, FETCH_SIZE x2 "
