@@ -246,8 +246,8 @@ def train_leg(args, dev, world: int, rank: int) -> dict:
            "tflop_per_step_per_gpu": round(flops / 1e12, 3),
            "tflops_per_s_per_gpu": round(flops / ms / 1e9, 1),
            "mfma_frac": round(flops / ms / 1e9 / MFMA_BF16_PEAK_TFLOPS, 4),
-           "parallelism": f"dp{world}" + (" (bucketed RCCL all-reduce overlapped with the HIP backward)"
-                                           if world > 1 else ""),
+           "parallelism": f"dp{world}" + (f" (bucketed {'RCCL' if args.backend == 'nccl' else args.backend} "
+                                           "all-reduce overlapped with the HIP backward)" if world > 1 else ""),
            "dtype": "bf16 storage, fp32 accumulation and master weights"}
     if world > 1:
         res["ms_per_step_no_allreduce"] = round(ms_local, 3)
@@ -293,7 +293,7 @@ def main():
         tmpl.load_state_dict(sd_cpu)  # raises unless the file is a ResNet(blocks, 0.2, xS) state_dict
         x_cpu, hr = heldout_tiles(n, hw, S, seed=HELDOUT_SEED + 7919 * rank)
         weights_desc = (f"trained ResNet({args.blocks}, 0.2, x{S}) ({Path(args.weights).name}: train.py --resnet on "
-                        "1/f^1.4 synthetic crops), held-out tiles of that distribution")
+                        "synthetic dead-leaves crops), held-out tiles of that distribution")
     gw = engine.pack_generator({k: v.to(dev) for k, v in sd_cpu.items()}, enchant=False, add_rate=0.2, device=dev)
     x = x_cpu.to(dev).contiguous()
     mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)

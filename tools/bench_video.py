@@ -48,6 +48,26 @@ def main():
     e1.record(up.stream)
     torch.cuda.synchronize()
     gpu_ms = e0.elapsed_time(e1) / reps
+    # the persistent trunk kernel alone (its launch replayed on the plan's stream): its share of
+    # the per-batch GPU time, and the batch's trunk FLOPs per second
+    import ctypes
+
+    from image_super_resolution_amd import ops
+    plan = up.plan.subs[0] if hasattr(up.plan, "subs") else up.plan
+    chain = getattr(plan, "chain", None)
+    trunk_ms = None
+    if chain is not None:
+        with torch.cuda.stream(up.stream):
+            sp = ops._stream()
+            t0e, t1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0e.record(up.stream)
+            for _ in range(reps):
+                chain.fn(ctypes.byref(chain.desc), sp)
+            t1e.record(up.stream)
+        torch.cuda.synchronize()
+        trunk_ms = t0e.elapsed_time(t1e) / reps
+        assert not chain.failed()
+    frame_flops = engine.generator_flops(args.height, args.width, args.blocks, 1)
     # end to end
     pipe = video.VideoUpscaler(up)
     rec = video.NullRecorder()
@@ -62,6 +82,11 @@ def main():
                       "unit": "frames/s", "frames": n, "batch": args.batch, "in": f"{args.width}x{args.height}",
                       "out": f"{W}x{H}", "graph": not args.no_graph,
                       "gpu_ms_per_batch": round(gpu_ms, 3), "gpu_fps": round(args.batch * 1e3 / gpu_ms, 3),
+                      "trunk": "persistent trunk kernel" if chain is not None else "per-conv launches",
+                      "trunk_ms_per_batch": None if trunk_ms is None else round(trunk_ms, 3),
+                      "trunk_share": None if trunk_ms is None else round(trunk_ms / gpu_ms, 4),
+                      "model_tflops_per_s": round(frame_flops * args.batch / gpu_ms / 1e9, 1),
+                      "tflop_per_frame": round(frame_flops / 1e12, 2),
                       "out_mpix_s": round(n * H * W / dt / 1e6, 1),
                       "data": "synthetic frames, synthetic weights, NullRecorder (no encoder)"}))
 
