@@ -347,11 +347,19 @@ def main():
         trunk_flops = args.blocks * 3 * (sum(2.0 * 9 * (64 + 32 * k) * 32 for k in range(4))
                                          + 2.0 * 9 * 192 * 64) * npx
         c_gbs = trunk_bytes / (c_ms * 1e-3) / 1e9
+        # what the kernel stages into LDS per launch: per (tile, 16-channel
+        # chunk) its 18 x 34 halo plane and the chunk's 32- / 64-cout weights, for every tile of every layer
+        tiles = n * (-(-hw // 16)) * (-(-hw // 32))
+        halo_b, wg_b, wf_b = 18 * 34 * 32, 9 * 32 * 16 * 2, 9 * 64 * 16 * 2
+        staged_halo = args.blocks * 3 * tiles * (sum(4 + 2 * k for k in range(4)) + 12) * halo_b
+        staged_w = args.blocks * 3 * tiles * (sum(4 + 2 * k for k in range(4)) * wg_b + 12 * wf_b)
         kernels["chain"] = {"bound": "hbm", "kernel": "trunk_kernel (trunk.hip: the RRDB trunk, 240 convs, one persistent launch)",
                             "achieved": round(c_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(c_gbs / HBM_PEAK_GBS, 4), "traffic": traffic.get("chain"),
                             "bytes_per_launch": trunk_bytes, "flops_per_launch": trunk_flops,
                             "avg_launch_ms": round(c_ms, 5), "launches_per_step": len(c_tags),
+                            "lds_staged_bytes_per_launch": {"halo": staged_halo, "weights": staged_w,
+                                                            "gb_s": round((staged_halo + staged_w) / (c_ms * 1e-3) / 1e9, 1)},
                             "mfma_frac": round(trunk_flops / (c_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
                             "share_of_step": round(c_ms / ms, 4)}
     iso = engine.GeneratorPlan(gw, n, hw, hw, dev, False, False, mean, std, chain=False)
