@@ -396,7 +396,7 @@ static int wgrad3x3_parts(const isr_wgrad_desc* d, int32_t variant, void* worksp
     int rc = wgrad_validate(d);
     if (rc != ISR_OK) return rc;
     if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null workspace");
-    if (variant < 0 || variant > 14) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: no variant %d", variant);
+    if (variant < 0 || variant > 15) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: no variant %d", variant);
     rc = isr::wgrad3x3_dispatch(d, variant, workspace, ws_bytes, (hipStream_t)s, parts);
     if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: workspace of %zu bytes is smaller than %zu", ws_bytes,
                               isr::wgrad3x3_workspace_bytes(d, variant));
@@ -453,7 +453,7 @@ int isr_wgrad3x3_reduce(const isr_wgrad_desc* d, void* workspace, size_t ws_byte
 }
 
 size_t isr_wgrad3x3_variant_workspace_bytes(const isr_wgrad_desc* d, int32_t variant) {
-    if (wgrad_validate(d) != ISR_OK || variant < 0 || variant > 14) return 0;
+    if (wgrad_validate(d) != ISR_OK || variant < 0 || variant > 15) return 0;
     return isr::wgrad3x3_workspace_bytes(d, variant);
 }
 

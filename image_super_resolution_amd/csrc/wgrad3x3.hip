@@ -24,6 +24,7 @@
 // layout (and un-permutes the PixelShuffle channel order for g_sub2).
 #include "isr_common.h"
 #include <cstdlib>
+#include <utility>
 
 namespace isr {
 
@@ -40,9 +41,49 @@ __device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int NCO_, int NCI_, int TY_, int KW_ = 1, int TWN_ = 0, int CW_ = 1, int NSTG_ = 2>
+// The same transposing read as inline asm at base + OFF, which hipcc does not see as an LDS load:
+// its waitcnt pass puts a vmcnt(0) in front of the first compiler-visible LDS read after a
+// global_load_lds (it cannot tell the stage being read from the one being filled), which made
+// every stage wait for the NEXT stage's DMA before computing.  The row sweep waits for these with
+// counted lgkmcnt waits of its own (lgk_wait) and ties the fragments to them (tie).
+template <int OFF>
+__device__ __forceinline__ bf16x4 tr4_at(uint32_t base) {
+    bf16x4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "i"(OFF) : "memory");
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void lgk_wait() {
+    static_assert(N >= 0 && N <= 15, "lgkmcnt range");
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+}
+__device__ __forceinline__ void tie(bf16x8& v) { asm volatile("" : "+v"(v)); }
+
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>)
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int NCO_, int NCI_, int TY_, int KW_ = 1, int TWN_ = 0, int CW_ = 1, int NSTG_ = 2, int RS_ = 0, int AR_ = 0>
 struct WG {
+    // AR = 1: the kernel-row form with the asm transposing reads (tr4_at) and counted waits, one
+    // K group read ahead; AR = 2 the same without read-ahead — the same MFMAs in the same order
+    // as AR = 0 (bit-identical)
+    static constexpr int AR = AR_;
     static constexpr int NCO = NCO_, NCI = NCI_, TY = TY_;
+    // row sweep (RS = 1): wave w owns kernel COLUMN dx = w % 3 and all three kernel rows, and walks
+    // the stage's halo rows once: X row rho is read once and feeds the taps (dy, dx) of G rows
+    // rho - dy, dy = 0..2 (the G fragments of the last three rows stay in registers).  Per 3 MFMAs
+    // that is one X + one G fragment instead of one G + three X fragments per 3 MFMAs (the
+    // default, wave = kernel row): the LDS read stream per MFMA halves.  Same operands, same
+    // per-tap summation order (G rows ascending) -> bit-identical partials.
+    static constexpr int RS = RS_;
+    static_assert(!RS_ || (TWN_ == 0 && KW_ == 2), "row sweep: 3x3 taps, one column half per K-share wave");
     // LDS stages in the pixel-tile ring: 2 (stage t+1 lands while stage t computes) or 3 (two
     // stages in flight: the weight-gradient loop had waited on its staging, PMC wait_any 0.48)
     static constexpr int NSTG = NSTG_;
@@ -96,7 +137,10 @@ __device__ __forceinline__ void wait_vm_upto15(uint32_t n) {
 
 // One block's work: (ci tile, co tile, split) = the block index b within its conv.
 template <class C>
-__device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, int splits, int tiles, int b) {
+__device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, int splits, int tiles, int b,
+                                           int abl = 0) {
+    // abl (tuning builds, timing probes, wrong results): 1 = no refill DMA after the first stage,
+    // 2 = no MFMAs (the row sweep's reads stay)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int NCO = C::NCO, NCI = C::NCI, TY = C::TY;
     const int ncot = d.cout / C::CO_T, ncit = d.cin / C::CI_T;
@@ -208,8 +252,145 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (t + C::NSTG - 1 < t1) stage(t + C::NSTG - 1, (t + C::NSTG - 1 - t0) % C::NSTG);
+        if (t + C::NSTG - 1 < t1 && !(abl & 1) && !(C::RS & 2)) stage(t + C::NSTG - 1, (t + C::NSTG - 1 - t0) % C::NSTG);
         const char* base = smem + cur * C::STAGE;
+        if constexpr (C::RS) {
+            // RS & 2: the next stage's LDS-DMA pieces go out one per halo row, between the row's
+            // fragment reads and its MFMAs (issued as one block at the top of the stage they held
+            // each wave's reads and MFMAs behind ~1,000 cycles of DMA issue); RS & 4: fragments
+            // read two rows ahead instead of one
+            const bool refill = t + C::NSTG - 1 < t1 && !(abl & 1);
+            const char *rgb = nullptr, *rxb = nullptr;
+            char* rdst = nullptr;
+            if constexpr ((C::RS & 2) != 0) {
+                const int tn = t + C::NSTG - 1;
+                const int bx = tn % nbx;
+                const int rq = tn / nbx;
+                const int y0 = (rq % nby) * TY, img = rq / nby, x0 = bx * 32;
+                rgb = d.g_sub2 ? view_at(d.g, img, 2 * y0, 2 * x0, 0) : view_at(d.g, img, y0, x0, 0);
+                rxb = d.x_sub2 ? view_at(d.x, img, 2 * (y0 - 1), 2 * (x0 - 1), 0) : view_at(d.x, img, y0 - 1, x0 - 1, 0);
+                rdst = smem + ((tn - t0) % C::NSTG) * C::STAGE;
+            }
+            auto piece = [&](auto K) {
+                constexpr int k = decltype(K)::value;
+                if constexpr ((C::RS & 2) != 0 && k < C::IPW) {
+                    const int j = wave + C::WM * k;
+                    if (refill && j < C::INSTR) glds16((j < C::G_INSTR ? rgb : rxb) + off[k], rdst + lds_dst(j));
+                }
+            };
+            // wave (dx = dy-slot, column half kh): halo rows rho = 0..TY+1, G rows r = rho - tap row;
+            // row rho+1's fragments are read while row rho's MFMAs run
+            const int c0 = kh * 16, dxw = dy;
+            const uint32_t ab = (uint32_t)(uintptr_t)ISR_LDS_PTR(base + a_lane + c0 * 32);
+            const uint32_t bb =
+                (uint32_t)(uintptr_t)ISR_LDS_PTR(base + b_lane + 2 * cw * NCIW * C::X_PLANE + (c0 + dxw) * 32);
+            bf16x8 ga[TY][NCO];
+            bf16x8 xb[TY + 2][NCIW];
+            auto issue = [&](auto R) {
+                constexpr int r = decltype(R)::value;
+                if constexpr (r < TY)
+                    sfor<NCO>([&](auto F) {
+                        constexpr int o = 2 * decltype(F)::value * C::G_PLANE + r * 32 * 32;
+                        ga[r][decltype(F)::value] = cat4(tr4_at<o>(ab), tr4_at<o + 4 * 32>(ab));
+                    });
+                sfor<NCIW>([&](auto E) {
+                    constexpr int o = 2 * decltype(E)::value * C::X_PLANE + r * 34 * 32;
+                    xb[r][decltype(E)::value] = cat4(tr4_at<o>(bb), tr4_at<o + 4 * 32>(bb));
+                });
+            };
+            constexpr int AH = (C::RS & 4) ? 2 : 1;  // rows read ahead
+            auto nrd = [](int r) constexpr { return r < TY + 2 ? 2 * NCIW + (r < TY ? 2 * NCO : 0) : 0; };
+            issue(std::integral_constant<int, 0>{});
+            if constexpr (AH == 2) issue(std::integral_constant<int, 1>{});
+            sfor<TY + 2>([&](auto R) {
+                constexpr int rho = decltype(R)::value;
+                if constexpr (rho + AH < TY + 2) issue(std::integral_constant<int, rho + AH>{});
+                piece(std::integral_constant<int, rho>{});
+                // row rho's reads landed (the younger rows' may stay in flight)
+                lgk_wait<nrd(rho + 1) + (AH == 2 ? nrd(rho + 2) : 0)>();
+                if constexpr (rho < TY) {
+#pragma unroll
+                    for (int f = 0; f < NCO; ++f) tie(ga[rho][f]);
+                    if (do_bias) {
+#pragma unroll
+                        for (int f = 0; f < NCO; ++f)
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) bsum[f] += (float)ga[rho][f][e];
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < NCIW; ++e) tie(xb[rho][e]);
+#pragma unroll
+                for (int ty = 0; ty < 3; ++ty) {
+                    const int r = rho - ty;
+                    if (r < 0 || r >= TY || (abl & 2)) continue;
+#pragma unroll
+                    for (int f = 0; f < NCO; ++f)
+#pragma unroll
+                        for (int e = 0; e < NCIW; ++e) acc[ty][f][e] = mfma32(ga[r][f], xb[rho][e], acc[ty][f][e]);
+                }
+            });
+            continue;
+        }
+        if constexpr (C::AR) {
+            // K group kk: pixel row r = kk * KW / 2 + (kh >> 1) and column half (kh & 1) for even KW,
+            // r = kk >> 1 and half kk & 1 for KW = 1; the run-time part goes into the base addresses
+            constexpr int KW = C::KW, NK = 2 * TY / KW, TN = C::TN;
+            const int rr = KW == 1 ? 0 : (kh >> 1), cr = KW == 1 ? 0 : (kh & 1) * 16;
+            const uint32_t ab = (uint32_t)(uintptr_t)ISR_LDS_PTR(base + a_lane + (rr * 32 + cr) * 32);
+            const uint32_t bb = (uint32_t)(uintptr_t)ISR_LDS_PTR(base + b_lane + 2 * cw * NCIW * C::X_PLANE +
+                                                                  ((rr + dy) * 34 + cr) * 32);
+            bf16x8 fa[NK][NCO];
+            bf16x8 fb[NK][TN][NCIW];
+            auto issue = [&](auto K) {
+                constexpr int kk = decltype(K)::value;
+                constexpr int rk = KW == 1 ? kk >> 1 : kk * KW / 2, ck = KW == 1 ? (kk & 1) * 16 : 0;
+                sfor<NCO>([&](auto F) {
+                    constexpr int o = 2 * decltype(F)::value * C::G_PLANE + (rk * 32 + ck) * 32;
+                    fa[kk][decltype(F)::value] = cat4(tr4_at<o>(ab), tr4_at<o + 4 * 32>(ab));
+                });
+                sfor<TN>([&](auto D) {
+                    sfor<NCIW>([&](auto E) {
+                        constexpr int o = 2 * decltype(E)::value * C::X_PLANE + (rk * 34 + ck + decltype(D)::value) * 32;
+                        fb[kk][decltype(D)::value][decltype(E)::value] = cat4(tr4_at<o>(bb), tr4_at<o + 4 * 32>(bb));
+                    });
+                });
+            };
+            constexpr int NR = 2 * NCO + 2 * TN * NCIW;  // reads per K group
+            issue(std::integral_constant<int, 0>{});
+            sfor<NK>([&](auto K) {
+                constexpr int kk = decltype(K)::value;
+                if constexpr (kk + 1 < NK && NR <= 15 && C::AR == 1) {
+                    issue(std::integral_constant<int, kk + 1>{});
+                    lgk_wait<NR>();
+                } else if constexpr (C::AR == 1) {
+                    lgk_wait<0>();
+                    if constexpr (kk + 1 < NK) issue(std::integral_constant<int, kk + 1>{});
+                } else {  // AR = 2: no read-ahead (one K group of fragments live: no spill at 64 x 96)
+                    if constexpr (kk > 0) issue(std::integral_constant<int, kk>{});
+                    lgk_wait<0>();
+                }
+#pragma unroll
+                for (int f = 0; f < NCO; ++f) tie(fa[kk][f]);
+#pragma unroll
+                for (int dx = 0; dx < TN; ++dx)
+#pragma unroll
+                    for (int e = 0; e < NCIW; ++e) tie(fb[kk][dx][e]);
+                if (do_bias) {
+#pragma unroll
+                    for (int f = 0; f < NCO; ++f)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) bsum[f] += (float)fa[kk][f][e];
+                }
+#pragma unroll
+                for (int dx = 0; dx < TN; ++dx)
+#pragma unroll
+                    for (int f = 0; f < NCO; ++f)
+#pragma unroll
+                        for (int e = 0; e < NCIW; ++e) acc[dx][f][e] = mfma32(fa[kk][f], fb[kk][dx][e], acc[dx][f][e]);
+            });
+            continue;
+        }
 #pragma unroll
         for (int kk = 0; kk < 2 * TY / C::KW; ++kk) {
             const int kg = kk * C::KW + kh;
@@ -286,7 +467,8 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
     float* wsp = ws + (size_t)split * (9 * d.cout * d.cin + d.cout);
 #pragma unroll
     for (int dx = 0; dx < C::TN; ++dx) {
-        float* wt = wsp + (size_t)(dy * 3 + dx) * d.cout * d.cin;
+        // accumulator slot dx = kernel column (default) or kernel row (row sweep; dy = the column)
+        float* wt = wsp + (size_t)(C::RS ? dx * 3 + dy : dy * 3 + dx) * d.cout * d.cin;
 #pragma unroll
         for (int f = 0; f < NCO; ++f)
 #pragma unroll
@@ -327,6 +509,7 @@ struct WgradGroupArgs {
     int pstart[WG_GROUP_MAX + 1];  // (co, ci) tile pairs
     int n, splits, tiles, pairs;
     int order;  // block order: 0 = member-major, 1 = split-major over all members' tile pairs
+    int abl;    // timing-probe ablations (tuning builds; 0 in production)
 };
 
 __device__ __forceinline__ int group_member(const WgradGroupArgs& g, const int* start, int b) {
@@ -353,7 +536,11 @@ __global__ __launch_bounds__(C::NT) void wgrad3x3_group_kernel(WgradGroupArgs g)
         t = group_member(g, g.start, l);
         b = l - g.start[t];
     }
+#ifdef ISR_TUNING
+    wgrad_body<C>(g.d[t], g.ws[t], g.splits, g.tiles, b, g.abl);
+#else
     wgrad_body<C>(g.d[t], g.ws[t], g.splits, g.tiles, b);
+#endif
 }
 
 // dW[co][ci][tap] (reference OIHW) = scale * sum_s ws[s][tap][co'][ci];  co' = kernel channel order.
@@ -577,6 +764,33 @@ static auto pick_cw(const isr_wgrad_desc* d, F&& f, bool* ok) {
     return f(Fam<4>::C11());
 }
 
+// AR = 1 (production): the asm-read forms (WG::AR / WG::RS); 0 = compiler-visible LDS reads;
+// the 64 x 96 final-conv tile reads without read-ahead (AR 2: 8 B of scratch with it)
+template <int AR, class F>
+static auto pick_default(const isr_wgrad_desc* d, F&& f) {
+    // the discriminator's wide layers (variant 14: -0.5 % per SRGAN step, same-box A/B): 64 co x
+    // 128 (or 64) ci per block, 8-12 waves splitting the ci tiles, each pixel tile staged once
+    if (d->cout % 64 == 0 && d->ha % 4 == 0 && !d->g_sub2) {
+        if (d->taps == 1 && d->cin % 128 == 0) return f(WG<2, 4, 4, 1, 1, 4, 2, 0, AR>());
+        if (d->taps == 0 && d->cout >= 128 && d->cin % 128 == 0) return f(WG<2, 4, 4, 1, 0, 4, 2, 0, AR>());
+        if (d->taps == 0 && d->cout >= 128 && d->cin % 64 == 0) return f(WG<2, 2, 4, 1, 0, 2, 2, 0, AR>());
+    }
+    if (d->taps == 1) return f(WG<1, 1, 8, 2, 1, 1, 2, 0, AR>());  // stride-2 phase conv: taps {0,1}^2, 4 waves
+    // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles; 4-row
+    // stages when cin % 64 == 32 (96, 160), else 8-row stages with 2 waves per kernel
+    // row (variant 5): 4-11 % under the round-1 choice (16-row stages, 4 waves per
+    // row) on cin 64 / 128 / 192 and the sub2 Scaler shape, on two boxes
+    // the RDB final conv (cin 192, cout 64): 64x96 (co, ci) per block, 9 waves splitting the
+    // ci tiles (each pixel tile staged once per block): 81-86 vs 98-104 us
+    if (d->cin == 192 && d->cout == 64 && !d->g_sub2 && !d->x_sub2 && d->ha % 4 == 0)
+        return f(WG<2, 3, 4, 1, 0, 3, 2, 0, AR ? 2 : 0>());
+    if (d->cin % 64 == 32) return f(WG<1, 1, 4, 1, 0, 1, 2, 0, AR>());
+    // 8-row stages, 2 waves per kernel row; with AR as the row sweep (WG::RS, same bits)
+    if (d->ha % 8 == 0) return f(WG<1, 1, 8, 2, 0, 1, 2, AR, 0>());
+    if (d->ha % 4 == 0) return f(WG<1, 1, 4, 1, 0, 1, 2, 0, AR>());
+    return f(WG<1, 1, 2, 1, 0, 1, 2, 0, AR>());
+}
+
 template <class F>
 static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
     switch (variant) {
@@ -606,31 +820,17 @@ static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
         case 9: return f(Fam<16, 4>::C11());          // 16-row stages, 4 waves per kernel row
         case 10: return f(Fam<4, 4>::C11());          // 4-row stages, 4 waves per kernel row
         case 11: return f(Fam<16, 2>::C11());         // 16-row stages, 2 waves per kernel row
+        case 15:                                      // variant 5 as a row sweep (WG::RS)
+            if (d->taps == 0 && d->ha % 8 == 0) return f(WG<1, 1, 8, 2, 0, 1, 2, 1>());
+            break;
         default: break;
     }
-    switch (0) {
-        default:
-            // the discriminator's wide layers (variant 14: -0.5 % per SRGAN step, same-box A/B): 64 co x
-            // 128 (or 64) ci per block, 8-12 waves splitting the ci tiles, each pixel tile staged once
-            if (d->cout % 64 == 0 && d->ha % 4 == 0 && !d->g_sub2) {
-                if (d->taps == 1 && d->cin % 128 == 0) return f(WG<2, 4, 4, 1, 1, 4>());
-                if (d->taps == 0 && d->cout >= 128 && d->cin % 128 == 0) return f(WG<2, 4, 4, 1, 0, 4>());
-                if (d->taps == 0 && d->cout >= 128 && d->cin % 64 == 0) return f(WG<2, 2, 4, 1, 0, 2>());
-            }
-            if (d->taps == 1) return f(WG<1, 1, 8, 2, 1>());  // stride-2 phase conv: taps {0,1}^2, 4 waves
-            // production (tools/tune_wgrad.py, MI355X, N=16 128²): 32x32 (co, ci) tiles; 4-row
-            // stages when cin % 64 == 32 (96, 160), else 8-row stages with 2 waves per kernel
-            // row (variant 5): 4-11 % under the round-1 choice (16-row stages, 4 waves per
-            // row) on cin 64 / 128 / 192 and the sub2 Scaler shape, on two boxes
-            // the RDB final conv (cin 192, cout 64): 64x96 (co, ci) per block, 9 waves splitting the
-            // ci tiles (each pixel tile staged once per block): 81-86 vs 98-104 us
-            if (d->cin == 192 && d->cout == 64 && !d->g_sub2 && !d->x_sub2 && d->ha % 4 == 0)
-                return f(WG<2, 3, 4, 1, 0, 3>());
-            if (d->cin % 64 == 32) return f(Fam<4>::C11());
-            if (d->ha % 8 == 0) return f(Fam<8, 2>::C11());
-            if (d->ha % 4 == 0) return f(Fam<4>::C11());
-            return f(Fam<2>::C11());
-    }
+#ifdef ISR_TUNING
+    // A/B of the kernel-row forms with compiler-visible LDS reads (tuning builds: ISR_WGRAD_AR=0)
+    static const bool ar = !getenv("ISR_WGRAD_AR") || atoi(getenv("ISR_WGRAD_AR")) != 0;
+    if (!ar) return pick_default<0>(d, f);
+#endif
+    return pick_default<1>(d, f);
 }
 
 size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d, int variant) {
@@ -694,7 +894,10 @@ static int group_plan(const isr_wgrad_desc* ds, int n, WgradGroupArgs* g, size_t
     // block order: split-major (1) in production; the pair-major A/B form (0) only in tuning
     // builds (both give the same bits: every block's partial and the reduce are unchanged)
     g->order = 1;
+    g->abl = 0;
 #ifdef ISR_TUNING
+    static const int abl_probe = getenv("ISR_WGRAD_ABLATE") ? atoi(getenv("ISR_WGRAD_ABLATE")) : 0;
+    g->abl = abl_probe;
     static const int order_probe = getenv("ISR_WGRAD_GROUP_ORDER") ? atoi(getenv("ISR_WGRAD_GROUP_ORDER")) : 1;
     g->order = order_probe;
 #endif
@@ -720,9 +923,18 @@ static auto group_pick(const isr_wgrad_desc* ds, int n, F&& f) {
     if (cfg == 5) return f(WG<1, 1, 4, 1, 0, 1, 3>());          // 4-row stages, 3-stage ring
     if (cfg == 6) return f(WG<1, 1, 4, 2, 0, 1, 3>());          // 4-row stages, 2 waves per row, 3 stages
     if (cfg == 7 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 3>());   // production tile, 3 stages (1 block / CU)
+    if (cfg == 8 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 1>());   // production tile, row sweep
+    if (cfg == 9 && ty16) return f(WG<1, 1, 16, 2, 0, 1, 2, 1>()); // 16-row stages, row sweep (1 block / CU)
+    if (cfg == 10 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 3, 1>());  // row sweep, 3 stages
+    if (cfg == 11 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 0, 1>());  // kernel-row form, asm reads
+    if (cfg == 12) return ty8 ? f(Fam<8, 2>::C11()) : f(Fam<4>::C11());  // round-4 production
+    if (cfg == 13 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 3>());  // row sweep + DMA one piece per row
+    if (cfg == 14 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 5>());  // row sweep, 2 rows read ahead
+    if (cfg == 15 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 7>());  // both
 #endif
     (void)ty16;
-    return ty8 ? f(Fam<8, 2>::C11()) : f(Fam<4>::C11());
+    // 8-row stages, 2 waves per kernel column: the row sweep (WG::RS)
+    return ty8 ? f(WG<1, 1, 8, 2, 0, 1, 2, 1>()) : f(WG<1, 1, 4, 1, 0, 1, 2, 0, 1>());
 }
 
 size_t wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* ds, int n) {
