@@ -84,6 +84,7 @@ struct WG {
     // per-tap summation order (G rows ascending) -> bit-identical partials.
     static constexpr int RS = RS_;
     static_assert(!RS_ || (TWN_ == 0 && KW_ == 2), "row sweep: 3x3 taps, one column half per K-share wave");
+    static_assert(!((RS_ & 2) && (RS_ & 8)), "per-row DMA pieces and loader waves exclude each other");
     // LDS stages in the pixel-tile ring: 2 (stage t+1 lands while stage t computes) or 3 (two
     // stages in flight: the weight-gradient loop had waited on its staging, PMC wait_any 0.48)
     static constexpr int NSTG = NSTG_;
@@ -96,7 +97,11 @@ struct WG {
     // KW waves per kernel row dy split each stage's K (pixel groups) between them;
     // their partial sums are added through LDS before the workspace store
     static constexpr int KW = KW_;
-    static constexpr int WM = TN * KW * CW, NT = 64 * WM;
+    // RS & 8: LW = 2 loader waves per block issue every LDS-DMA piece (the compute waves issue
+    // none: their reads and MFMAs no longer queue behind ~7 DMA issues per stage)
+    static constexpr int LW = (RS_ & 8) ? 2 : 0;
+    static constexpr int WM = TN * KW * CW, NT = 64 * (WM + LW);
+    static constexpr int SW = LW ? LW : WM;  // waves that stage
     static_assert(NCI % CW == 0, "ci tiles split evenly between the CW waves");
     static constexpr int CO_T = 32 * NCO, CI_T = 32 * NCI;
     static constexpr int GPL = 2 * NCO, XPL = 2 * NCI;         // 16-channel planes per stage
@@ -110,7 +115,7 @@ struct WG {
     static constexpr int G_BYTES = GPL * G_PLANE;
     static constexpr int STAGE = G_BYTES + XPL * X_PLANE;
     static constexpr int G_INSTR = GPL * G_IPL, INSTR = G_INSTR + XPL * X_IPL;
-    static constexpr int IPW = (INSTR + WM - 1) / WM;
+    static constexpr int IPW = (INSTR + SW - 1) / SW;
     static constexpr int RED = CW * (KW - 1) * TN * 64 * (TN * NCO * NCIW * 16 + NCO) * 4;  // cross-wave K reduction
     static constexpr int LDS = NSTG * STAGE > RED ? NSTG * STAGE : RED;
     static_assert(LDS <= 163840, "LDS budget");
@@ -149,6 +154,9 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
     const int split = b;
     const int t0 = (int)((long)split * tiles / splits), t1 = (int)((long)(split + 1) * tiles / splits);
     const int wave = wave_id();
+    const bool loader = C::LW && wave >= C::WM;                  // RS & 8: a DMA-only wave
+    const bool stager = !C::LW || loader;
+    const int sw = C::LW ? wave - C::WM : wave;                  // index among the staging waves
     const int dy = wave % C::TN, kh = (wave / C::TN) % C::KW;  // kernel row, K-share of this wave
     const int cw = wave / (C::TN * C::KW);                       // ci-tile group of this wave
     constexpr int NCIW = C::NCIW;
@@ -162,7 +170,7 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
     uint32_t off[C::IPW];
 #pragma unroll
     for (int k = 0; k < C::IPW; ++k) {
-        const int j = wave + C::WM * k;
+        const int j = sw + C::SW * k;
         uint32_t o = 0;
         if (j < C::G_INSTR) {
             const int pl = j / C::G_IPL, rr = j - pl * C::G_IPL;
@@ -212,8 +220,8 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
         char* dst = smem + buf * C::STAGE;
 #pragma unroll
         for (int k = 0; k < C::IPW; ++k) {
-            const int j = wave + C::WM * k;
-            if (j < C::INSTR) glds16((j < C::G_INSTR ? gb : xb) + off[k], dst + lds_dst(j));
+            const int j = sw + C::SW * k;
+            if (stager && j >= 0 && j < C::INSTR) glds16((j < C::G_INSTR ? gb : xb) + off[k], dst + lds_dst(j));
         }
     };
 
@@ -229,7 +237,7 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
     float bsum[NCO];
 #pragma unroll
     for (int f = 0; f < NCO; ++f) bsum[f] = 0.f;
-    const bool do_bias = d.db && cit == 0 && dy == 1 && cw == 0;
+    const bool do_bias = d.db && cit == 0 && dy == 1 && cw == 0 && !loader;
 
     // transposed-read lane geometry: plane gi of the 32-channel fragment, pixel q + 8h, channels 4p..4p+3
     const int gi = (lane >> 4) & 1, hh = lane >> 5, q = (lane >> 2) & 3, p = lane & 3;
@@ -237,7 +245,7 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
     const int b_lane = C::G_BYTES + gi * C::X_PLANE + (8 * hh + q) * 32 + 8 * p;
 
     // this wave's copies per stage (wave-uniform)
-    const int nps = (C::INSTR - wave + C::WM - 1) / C::WM < C::IPW ? (C::INSTR - wave + C::WM - 1) / C::WM : C::IPW;
+    const int nps = (C::INSTR - sw + C::SW - 1) / C::SW < C::IPW ? (C::INSTR - sw + C::SW - 1) / C::SW : C::IPW;
 #pragma unroll
     for (int s0 = 0; s0 < C::NSTG - 1; ++s0)
         if (t0 + s0 < t1) stage(t0 + s0, s0);
@@ -253,6 +261,7 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (t + C::NSTG - 1 < t1 && !(abl & 1) && !(C::RS & 2)) stage(t + C::NSTG - 1, (t + C::NSTG - 1 - t0) % C::NSTG);
+        if (loader) continue;  // RS & 8: the loader waves only stage
         const char* base = smem + cur * C::STAGE;
         if constexpr (C::RS) {
             // RS & 2: the next stage's LDS-DMA pieces go out one per halo row, between the row's
@@ -274,8 +283,8 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
             auto piece = [&](auto K) {
                 constexpr int k = decltype(K)::value;
                 if constexpr ((C::RS & 2) != 0 && k < C::IPW) {
-                    const int j = wave + C::WM * k;
-                    if (refill && j < C::INSTR) glds16((j < C::G_INSTR ? rgb : rxb) + off[k], rdst + lds_dst(j));
+                    const int j = sw + C::SW * k;
+                    if (refill && stager && j >= 0 && j < C::INSTR) glds16((j < C::G_INSTR ? rgb : rxb) + off[k], rdst + lds_dst(j));
                 }
             };
             // wave (dx = dy-slot, column half kh): halo rows rho = 0..TY+1, G rows r = rho - tap row;
@@ -429,7 +438,7 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
         __syncthreads();
         constexpr int PER = C::TN * NCO * NCIW * 16 + NCO;  // floats per lane
         float* red = reinterpret_cast<float*>(smem);
-        if (kh > 0) {
+        if (kh > 0 && !loader) {
             float* dst = red + ((size_t)((cw * (C::KW - 1) + kh - 1) * C::TN + dy) * 64 + lane) * PER;
             int q = 0;
 #pragma unroll
@@ -444,7 +453,7 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
             for (int f = 0; f < NCO; ++f) dst[q++] = bsum[f];
         }
         __syncthreads();
-        if (kh > 0) return;
+        if (kh > 0 || loader) return;
 #pragma unroll
         for (int k = 1; k < C::KW; ++k) {
             const float* src = red + ((size_t)((cw * (C::KW - 1) + k - 1) * C::TN + dy) * 64 + lane) * PER;
@@ -462,6 +471,7 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
         }
     }
 
+    if (loader) return;  // (KW == 1 forms: the loader waves leave after the loop)
     // ---- partial sums: ws[split][tap][co][ci], D[co = (g&3)+8(g>>2)+4h][ci = l31]
     const int l31 = lane & 31;
     float* wsp = ws + (size_t)split * (9 * d.cout * d.cin + d.cout);
@@ -931,6 +941,8 @@ static auto group_pick(const isr_wgrad_desc* ds, int n, F&& f) {
     if (cfg == 13 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 3>());  // row sweep + DMA one piece per row
     if (cfg == 14 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 5>());  // row sweep, 2 rows read ahead
     if (cfg == 15 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 7>());  // both
+    if (cfg == 16 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 9>());  // row sweep + 2 loader waves
+    if (cfg == 17 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 13>()); // + 2 rows read ahead
 #endif
     (void)ty16;
     // 8-row stages, 2 waves per kernel column: the row sweep (WG::RS)

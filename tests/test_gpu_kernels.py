@@ -399,6 +399,36 @@ def test_wgrad3x3_group_rdb_vs_autograd(n, h, w):
     assert lib.isr_wgrad3x3_group_workspace_bytes(arr2, 5) == 0
 
 
+@pytest.mark.parametrize("cin,cout,variant", [(64, 32, 5), (128, 32, 5), (96, 32, 2), (192, 64, 12),
+                                              (128, 128, 14), (128, 256, 14)])
+def test_wgrad3x3_row_sweep_and_asm_reads_bitwise(cin, cout, variant):
+    """Round 5: the production forms (row sweep WG::RS for 8-row 32x32 tiles; asm transposing reads
+    WG::AR for the kernel-row forms) against the round-4 form of the same tile and split count
+    (isr_wgrad3x3_variant): the same MFMAs on the same operands in the same order, so dW / db are
+    bit-identical."""
+    import ctypes
+    from image_super_resolution_amd import _lib, ops
+    lib = _lib.load()
+    n, h, w = 2, 40, 72
+    xb = ops.ActBuffer.from_nchw(bf(_mk(n, cin, h, w, 91)), pad=1)
+    gb = ops.ActBuffer.from_nchw(bf(_mk(n, cout, h, w, 92)), pad=1)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    res = []
+    for v in (0, variant):
+        dw = torch.full((cout, cin, 3, 3), float("nan"), device=DEV)
+        db = torch.full((cout,), float("nan"), device=DEV)
+        d = ops.wgrad3x3_desc(xb, cin, gb, cout, dw, db, scale=0.25)
+        nb = lib.isr_wgrad3x3_variant_workspace_bytes(ctypes.byref(d), v)
+        assert nb > 0
+        ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
+        assert lib.isr_wgrad3x3_variant(ctypes.byref(d), v, ws.data_ptr(), nb, st) == 0
+        torch.cuda.synchronize()
+        res.append((dw, db))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    rw, rb = _wgrad_ref(xb.to_nchw(0, cin), gb.to_nchw(0, cout), 0.25)
+    _close_rel(res[0][0], rw, 1e-3)
+
+
 def test_wgrad3x3_partials_then_reduce_equals_one_call():
     """isr_wgrad3x3_partials + isr_wgrad3x3_reduce (the reduce on another stream) == isr_wgrad3x3,
     bit for bit (same partition, same summation order)."""

@@ -99,6 +99,12 @@ def main():
         keys = {"copy_", "fill_", "zero_", "clone", "add_", "add", "mul", "mul_", "sub", "div", "_to_copy", "cat",
                 "stack", "zeros_like", "ones_like", "where", "abs", "sum", "mean"}
         root = str(Path(__file__).resolve().parents[1])
+        # ISR_TORCH_PROFILE_ALL=1: every aten op that may launch a kernel, sorted by count
+        ALL = os.environ.get("ISR_TORCH_PROFILE_ALL") == "1"
+        NOLAUNCH = {"view", "_unsafe_view", "reshape", "as_strided", "t", "permute", "detach", "expand", "slice",
+                    "select", "alias", "empty", "empty_strided", "empty_like", "unsqueeze", "squeeze", "transpose",
+                    "split", "split_with_sizes", "unbind", "new_empty", "new_empty_strided", "set_", "lift_fresh",
+                    "_local_scalar_dense", "is_nonzero", "resolve_conj", "resolve_neg", "record_stream"}
 
         class _Count(TorchDispatchMode):
             def __init__(self):
@@ -108,7 +114,7 @@ def main():
 
             def __torch_dispatch__(self, func, types, args=(), kwargs=None):
                 name = func.overloadpacket.__name__
-                if name in keys:
+                if name in keys or (ALL and name not in NOLAUNCH):
                     fr = [f for f in traceback.extract_stack()[:-1]
                           if f.filename.startswith(root) and "bench_train" not in f.filename]
                     site = " <- ".join(f"{Path(f.filename).name}:{f.lineno}" for f in fr[::-1][:3])
@@ -121,7 +127,8 @@ def main():
         with mode:
             run(args.steps)
             torch.cuda.synchronize()
-        for (name, site), c in sorted(mode.n.items(), key=lambda kv: -mode.bytes[kv[0]])[:40]:
+        order = (lambda kv: -kv[1]) if ALL else (lambda kv: -mode.bytes[kv[0]])
+        for (name, site), c in sorted(mode.n.items(), key=order)[:60]:
             print(f"{c / args.steps:7.1f}/step {mode.bytes[(name, site)] / args.steps / 2**20:10.1f} MiB/step "
                   f"{name:10s} {site}")
         return
