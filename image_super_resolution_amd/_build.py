@@ -100,8 +100,30 @@ def build_interleave(verbose: bool = False) -> Path:
     return lib_path
 
 
+def build_probe16(verbose: bool = False) -> Path:
+    """libisr_probe16.so: production objects, trunk.hip with -DISR_TRUNK_MFMA16_PROBE=1 (timing
+    probe, outputs wrong: each growth-chunk MFMA as two 16x16x32 of the same FLOPs)."""
+    build(verbose=verbose)
+    objdir = PKG / "build_probe16"
+    objdir.mkdir(exist_ok=True)
+    trunk_obj = objdir / "trunk.o"
+    cmd = [HIPCC, *FLAGS, "-DISR_TRUNK_MFMA16_PROBE=1", "-c", str(CSRC / "trunk.hip"), "-o", str(trunk_obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed on trunk.hip (probe16):\n{r.stderr}")
+    objs = [trunk_obj if src.stem == "trunk" else PKG / "build" / (src.stem + ".o") for src in sources()]
+    lib_path = LIBDIR / "libisr_probe16.so"
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib_path), *map(str, objs)],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return lib_path
+
+
 if __name__ == "__main__":
-    if "--interleave" in sys.argv:
+    if "--probe16" in sys.argv:
+        print(build_probe16(verbose=True))
+    elif "--interleave" in sys.argv:
         print(build_interleave(verbose=True))
     else:
         print(build(force="--force" in sys.argv, verbose=True, tuning="--tuning" in sys.argv))

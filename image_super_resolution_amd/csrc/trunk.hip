@@ -151,6 +151,17 @@ __device__ __forceinline__ void trunk_stamp(int L, int t, int ntiles, int slot) 
 #endif
 }
 
+#if ISR_TRUNK_MFMA16_PROBE
+__device__ __forceinline__ f32x16 mfma32_probe16(bf16x8 a, bf16x8 b, f32x16 acc) {
+    f32x4 c0 = __builtin_shufflevector(acc, acc, 0, 1, 2, 3), c1 = __builtin_shufflevector(acc, acc, 4, 5, 6, 7);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c1, 0, 0, 0);
+    f32x4 c2 = __builtin_shufflevector(acc, acc, 8, 9, 10, 11), c3 = __builtin_shufflevector(acc, acc, 12, 13, 14, 15);
+    f32x8 lo = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7), hi = __builtin_shufflevector(c2, c3, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+}
+#endif
+
 // Tuning builds: ablation knobs (timing only, outputs wrong): bit 1 = no halo LDS-DMA after the
 // first item, 4 = no epilogue stores, 8 = no weight LDS-DMA, 16 = no dependency waits;
 // [1] = workgroups per CU (host side, 0 = occupancy).  (An MFMA ablation branch inside the step
@@ -726,6 +737,13 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                     }
     #pragma unroll
                     for (int r = 0; r < R; ++r) {
+#if ISR_TRUNK_MFMA16_PROBE
+                        // timing probe (lib/libisr_probe16.so, outputs wrong): each growth-chunk
+                        // 32x32x16 MFMA replaced by two 16x16x32 of the same FLOPs on the same operands
+                        if constexpr (NF == 1) {
+                            acc[r][0] = mfma32_probe16(fb[cur][dyi][0], fa[cur][r + dyi], acc[r][0]);
+                        } else
+#endif
     #pragma unroll
                         for (int f = 0; f < NF; ++f) acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][r + dyi], acc[r][f]);
                         if constexpr (NF == 2 && FC >= 0) {
