@@ -246,6 +246,13 @@ __device__ __forceinline__ void wgrad_body(const isr_wgrad_desc& d, float* ws, i
 
     // this wave's copies per stage (wave-uniform)
     const int nps = (C::INSTR - sw + C::SW - 1) / C::SW < C::IPW ? (C::INSTR - sw + C::SW - 1) / C::SW : C::IPW;
+    if (abl & 12) {
+        // timing probe (tuning builds): half the blocks start ~half a stage later (4 = the second
+        // 256 dispatched blocks, 8 = odd blocks), so co-resident blocks are not in phase
+        const bool late = (abl & 4) ? ((blockIdx.x >> 8) & 1) : (blockIdx.x & 1);
+        if (late)
+            for (int i = 0; i < 56; ++i) __builtin_amdgcn_s_sleep(1);
+    }
 #pragma unroll
     for (int s0 = 0; s0 < C::NSTG - 1; ++s0)
         if (t0 + s0 < t1) stage(t0 + s0, s0);
