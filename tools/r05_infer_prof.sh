@@ -12,9 +12,11 @@ f = glob.glob('/tmp/inftrace/**/inf_kernel_trace.csv', recursive=True) + glob.gl
 rows = list(csv.DictReader(open(f[0])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 t0 = int(rows[0]['Start_Timestamp'])
+tr = [i for i, r in enumerate(rows) if 'trunk_kernel' in r['Kernel_Name']]
+sel = rows[max(0, tr[4] - 12):tr[6] + 12] if len(tr) >= 7 else rows[-400:]
 with open('gpurun_out/r05/infer_trace.csv', 'w') as o:
     o.write('start_ns,dur_ns,queue,grid,wg,name\n')
-    for r in rows[-400:]:
+    for r in sel:
         o.write('%d,%d,%s,%s,%s,"%s"\n' % (int(r['Start_Timestamp']) - t0, int(r['End_Timestamp']) - int(r['Start_Timestamp']),
                                           r.get('Queue_Id', ''), r['Grid_Size_X'], r['Workgroup_Size_X'], r['Kernel_Name'][:120]))
 print(len(rows))
