@@ -61,3 +61,28 @@ def test_gpu_transform_lr_matches_cv2_linear_u8():
             x = crops.numpy().astype(np.float32)
             ref_hr = (x / 255.0 - mean) / std if hr_norm else 2.0 * (x / 255.0) - 1.0
             np.testing.assert_allclose(hr.numpy(), ref_hr, rtol=0, atol=2e-6)
+
+
+def test_heldout_tiles_do_not_depend_on_n():
+    """The trained-weight parity bar (tests/test_gpu_trained.py, bench.py parity) draws tile i from
+    its own generator, so the first tiles of a longer draw are the same tiles bit for bit."""
+    from image_super_resolution_amd.weights import heldout_tiles
+    lr2, hr2 = heldout_tiles(2, lr_size=32, scale=4)
+    lr3, hr3 = heldout_tiles(3, lr_size=32, scale=4)
+    assert lr2.shape == (2, 3, 32, 32) and hr2.shape == (2, 3, 128, 128)
+    assert torch.equal(lr2, lr3[:2]) and torch.equal(hr2, hr3[:2])
+    assert not torch.equal(hr3[1], hr3[2])  # distinct tiles
+    # HR is uint8-exact in [0, 1]; LR is the rounded bilinear resize of it, normalised
+    assert torch.equal((hr3 * 255).round() / 255, hr3)
+
+
+def test_leaves_images_have_edges_and_full_range():
+    """Dead-leaves crops (the trained weights' distribution): opaque discs give sharp edges (large
+    neighbour differences on a few pixels) over a wide intensity range."""
+    from image_super_resolution_amd.data import leaves_hr_u8
+    x = leaves_hr_u8(2, 96, torch.Generator().manual_seed(5), device="cpu").float()
+    assert x.dtype == torch.float32 and x.shape == (2, 3, 96, 96)
+    assert x.min() < 40 and x.max() > 215
+    d = (x[..., 1:] - x[..., :-1]).abs()
+    assert (d > 60).float().mean() > 0.002  # edges
+    assert (d < 8).float().mean() > 0.5     # mostly flat or smooth inside the discs
