@@ -30,6 +30,11 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-
          "-I", str(ROOT / "include"), "-I", str(CSRC)]
 
 
+# sources whose kernels read LDS through inline asm with hand-counted waits: their device assembly
+# is checked on every full build (tools/check_lds_waits.py)
+WAIT_CHECKED = ("wgrad3x3.hip", "conv9x9.hip")
+
+
 def sources() -> list[Path]:
     return sorted(CSRC.glob("*.hip"))
 
@@ -68,8 +73,25 @@ def build(force: bool = False, verbose: bool = False, tuning: bool = False) -> P
             print(r.stderr, file=sys.stderr)
         return obj
 
-    with ThreadPoolExecutor(max_workers=min(8, len(sources()))) as ex:
+    def check_waits(src: Path) -> list[str]:
+        """the hand-counted LDS waits of the asm-read kernels, checked on the gfx950
+        assembly hipcc produces for them (tools/check_lds_waits.py: no read of an LDS destination
+        before its wait, no SMEM load under a counted wait, no scratch)."""
+        sys.path.insert(0, str(ROOT / "tools"))
+        try:
+            import check_lds_waits
+        finally:
+            sys.path.pop(0)
+        asm = check_lds_waits.device_asm(src, ["-DISR_TUNING"] if tuning else [])
+        return check_lds_waits.check_asm(asm, src.name)
+
+    checked = [CSRC / n for n in WAIT_CHECKED] if (force or tuning or not LIB.exists()) else []
+    with ThreadPoolExecutor(max_workers=min(8, len(sources()) + len(checked))) as ex:
+        waits = [ex.submit(check_waits, src) for src in checked]
         objs = list(ex.map(compile_one, sources()))
+        errs = [e for w in waits for e in w.result()]
+    if errs:
+        raise RuntimeError("LDS wait check failed (tools/check_lds_waits.py):\n" + "\n".join(errs))
     tmp = lib_path.with_suffix(".so.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)

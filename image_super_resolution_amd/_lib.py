@@ -115,6 +115,7 @@ SIGNATURES = {
     "isr_wgrad3x3_partials": (c_int32, [POINTER(IsrWgradDesc), c_void_p, c_size_t, c_void_p]),
     "isr_wgrad3x3_group_workspace_bytes": (c_size_t, [POINTER(IsrWgradDesc), c_int32]),
     "isr_wgrad3x3_group": (c_int32, [POINTER(IsrWgradDesc), c_int32, c_void_p, c_size_t, c_void_p]),
+    "isr_wgrad3x3_group_variant": (c_int32, [POINTER(IsrWgradDesc), c_int32, c_int32, c_void_p, c_size_t, c_void_p]),
     "isr_wgrad3x3_reduce": (c_int32, [POINTER(IsrWgradDesc), c_void_p, c_size_t, c_void_p]),
     "isr_wgrad3x3_variant_workspace_bytes": (c_size_t, [POINTER(IsrWgradDesc), c_int32]),
     "isr_wgrad3x3_variant": (c_int32, [POINTER(IsrWgradDesc), c_int32, c_void_p, c_size_t, c_void_p]),

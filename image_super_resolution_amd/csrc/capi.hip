@@ -44,8 +44,8 @@ size_t wgrad3x3_workspace_bytes(const isr_wgrad_desc* d, int variant);
 size_t wgrad9x9_workspace_bytes(const isr_wgrad9_desc* d);
 int wgrad9x9_dispatch(const isr_wgrad9_desc* d, void* ws, size_t ws_bytes, hipStream_t s);
 int wgrad3x3_dispatch(const isr_wgrad_desc* d, int variant, void* ws, size_t ws_bytes, hipStream_t s, int parts);
-size_t wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* ds, int n);
-int wgrad3x3_group_dispatch(const isr_wgrad_desc* ds, int n, void* ws, size_t ws_bytes, hipStream_t s);
+size_t wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* ds, int n, int variant);
+int wgrad3x3_group_dispatch(const isr_wgrad_desc* ds, int n, void* ws, size_t ws_bytes, hipStream_t s, int variant);
 int mt_adam_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, const isr_adam_args* a,
                      const float* scale, const uint32_t* guard, hipStream_t s);
 int mt_sumsq_dispatch(const isr_mt_tensor* ts, const isr_mt_chunk* cs, int n, float* partial, hipStream_t s);
@@ -391,12 +391,23 @@ size_t isr_wgrad3x3_workspace_bytes(const isr_wgrad_desc* d) {
     return isr::wgrad3x3_workspace_bytes(d, 0);
 }
 
+// production: 0 and 16 (the compiler-read reference of the same tiles); tuning builds also 1-15
+static bool wgrad_variant_built(int32_t variant) {
+#ifdef ISR_TUNING
+    return variant >= 0 && variant <= 16;
+#else
+    return variant == 0 || variant == 16;
+#endif
+}
+
 static int wgrad3x3_parts(const isr_wgrad_desc* d, int32_t variant, void* workspace, size_t ws_bytes,
                           isr_stream_t s, int parts) {
     int rc = wgrad_validate(d);
     if (rc != ISR_OK) return rc;
     if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: null workspace");
-    if (variant < 0 || variant > 15) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: no variant %d", variant);
+    if (!wgrad_variant_built(variant)) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3: no variant %d in this library%s",
+                                                   variant, variant >= 1 && variant <= 15 ? " (tuning form: build with "
+                                                   "-DISR_TUNING)" : "");
     rc = isr::wgrad3x3_dispatch(d, variant, workspace, ws_bytes, (hipStream_t)s, parts);
     if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad3x3: workspace of %zu bytes is smaller than %zu", ws_bytes,
                               isr::wgrad3x3_workspace_bytes(d, variant));
@@ -430,18 +441,24 @@ static int wgrad_group_validate(const isr_wgrad_desc* ds, int32_t n) {
 
 size_t isr_wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* descs, int32_t n) {
     if (wgrad_group_validate(descs, n) != ISR_OK) return 0;
-    return isr::wgrad3x3_group_workspace_bytes(descs, n);
+    return isr::wgrad3x3_group_workspace_bytes(descs, n, 0);
 }
 
-int isr_wgrad3x3_group(const isr_wgrad_desc* descs, int32_t n, void* workspace, size_t ws_bytes, isr_stream_t s) {
+int isr_wgrad3x3_group_variant(const isr_wgrad_desc* descs, int32_t n, int32_t variant, void* workspace,
+                               size_t ws_bytes, isr_stream_t s) {
     int rc = wgrad_group_validate(descs, n);
     if (rc != ISR_OK) return rc;
     if (!workspace) return fail(ISR_ERR_BAD_DESC, "wgrad3x3 group: null workspace");
-    rc = isr::wgrad3x3_group_dispatch(descs, n, workspace, ws_bytes, (hipStream_t)s);
+    if (variant != 0 && variant != 1) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3 group: no variant %d", variant);
+    rc = isr::wgrad3x3_group_dispatch(descs, n, workspace, ws_bytes, (hipStream_t)s, variant);
     if (rc == -3) return fail(ISR_ERR_BAD_DESC, "wgrad3x3 group: workspace of %zu bytes is smaller than %zu", ws_bytes,
-                              isr::wgrad3x3_group_workspace_bytes(descs, n));
+                              isr::wgrad3x3_group_workspace_bytes(descs, n, variant));
     if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "wgrad3x3 group: a member's cout / cin / ha does not fit the tile");
     return launched(rc, "wgrad3x3 group");
+}
+
+int isr_wgrad3x3_group(const isr_wgrad_desc* descs, int32_t n, void* workspace, size_t ws_bytes, isr_stream_t s) {
+    return isr_wgrad3x3_group_variant(descs, n, 0, workspace, ws_bytes, s);
 }
 
 int isr_wgrad3x3_partials(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s) {
@@ -453,7 +470,7 @@ int isr_wgrad3x3_reduce(const isr_wgrad_desc* d, void* workspace, size_t ws_byte
 }
 
 size_t isr_wgrad3x3_variant_workspace_bytes(const isr_wgrad_desc* d, int32_t variant) {
-    if (wgrad_validate(d) != ISR_OK || variant < 0 || variant > 15) return 0;
+    if (wgrad_validate(d) != ISR_OK || !wgrad_variant_built(variant)) return 0;
     return isr::wgrad3x3_workspace_bytes(d, variant);
 }
 

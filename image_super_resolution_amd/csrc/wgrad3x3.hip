@@ -808,8 +808,13 @@ static auto pick_default(const isr_wgrad_desc* d, F&& f) {
     return f(WG<1, 1, 2, 1, 0, 1, 2, 0, AR>());
 }
 
+// variant 0: the production pick; 16: the same tiles and split counts with compiler-visible LDS
+// reads (pick_default<0>: the reference the asm-read / row-sweep forms must equal bit for bit,
+// tests/test_gpu_kernels.py); 1-15: earlier tile forms, tuning builds only (-DISR_TUNING)
 template <class F>
 static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
+    if (variant == 16) return pick_default<0>(d, f);
+#ifdef ISR_TUNING
     switch (variant) {
         case 14: {  // ci-split forms for the discriminator's wide layers (64 co x 128 ci per block)
             if (d->cout % 64 == 0 && d->ha % 4 == 0) {
@@ -842,7 +847,6 @@ static auto wgrad_pick(const isr_wgrad_desc* d, int variant, F&& f) {
             break;
         default: break;
     }
-#ifdef ISR_TUNING
     // A/B of the kernel-row forms with compiler-visible LDS reads (tuning builds: ISR_WGRAD_AR=0)
     static const bool ar = !getenv("ISR_WGRAD_AR") || atoi(getenv("ISR_WGRAD_AR")) != 0;
     if (!ar) return pick_default<0>(d, f);
@@ -922,8 +926,10 @@ static int group_plan(const isr_wgrad_desc* ds, int n, WgradGroupArgs* g, size_t
     return 0;
 }
 
+// variant 0: production (the row sweep, or the asm-read 4-row form); 1: the same tiles and split
+// counts with compiler-visible LDS reads (bit-identical reference, tests/test_gpu_kernels.py)
 template <class F>
-static auto group_pick(const isr_wgrad_desc* ds, int n, F&& f) {
+static auto group_pick(const isr_wgrad_desc* ds, int n, F&& f, int variant = 0) {
     bool ty8 = true, ty16 = true;
     for (int t = 0; t < n; ++t) {
         ty8 = ty8 && ds[t].ha % 8 == 0;
@@ -952,19 +958,20 @@ static auto group_pick(const isr_wgrad_desc* ds, int n, F&& f) {
     if (cfg == 17 && ty8) return f(WG<1, 1, 8, 2, 0, 1, 2, 13>()); // + 2 rows read ahead
 #endif
     (void)ty16;
+    if (variant == 1) return ty8 ? f(WG<1, 1, 8, 2, 0, 1, 2, 0, 0>()) : f(WG<1, 1, 4, 1, 0, 1, 2, 0, 0>());
     // 8-row stages, 2 waves per kernel column: the row sweep (WG::RS)
     return ty8 ? f(WG<1, 1, 8, 2, 0, 1, 2, 1>()) : f(WG<1, 1, 4, 1, 0, 1, 2, 0, 1>());
 }
 
-size_t wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* ds, int n) {
+size_t wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* ds, int n, int variant) {
     return group_pick(ds, n, [&](auto c) -> size_t {
         WgradGroupArgs g;
         size_t bytes = 0;
         return group_plan<decltype(c)>(ds, n, &g, &bytes) == 0 ? bytes : 0;
-    });
+    }, variant);
 }
 
-int wgrad3x3_group_dispatch(const isr_wgrad_desc* ds, int n, void* ws, size_t ws_bytes, hipStream_t s) {
+int wgrad3x3_group_dispatch(const isr_wgrad_desc* ds, int n, void* ws, size_t ws_bytes, hipStream_t s, int variant) {
     return group_pick(ds, n, [&](auto c) -> int {
         using C = decltype(c);
         WgradGroupArgs g;
@@ -979,7 +986,7 @@ int wgrad3x3_group_dispatch(const isr_wgrad_desc* ds, int n, void* ws, size_t ws
         if (hipGetLastError() != hipSuccess) return -1;
         hipLaunchKernelGGL(wgrad_reduce_group_kernel, dim3(g.rstart[n]), dim3(256), 0, s, g);
         return hipGetLastError() == hipSuccess ? 0 : -1;
-    });
+    }, variant);
 }
 
 }  // namespace isr

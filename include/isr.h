@@ -190,10 +190,17 @@ int isr_wgrad3x3(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_
  * isr_wgrad3x3_group_workspace_bytes(descs, n) bytes. */
 size_t isr_wgrad3x3_group_workspace_bytes(const isr_wgrad_desc* descs, int32_t n);
 int isr_wgrad3x3_group(const isr_wgrad_desc* descs, int32_t n, void* workspace, size_t ws_bytes, isr_stream_t s);
+/* The grouped launch by an explicit form: 0 = production (isr_wgrad3x3_group: asm transposing
+ * LDS reads with counted waits), 1 = the same tiles and splits with compiler-visible LDS reads
+ * (the bit-identical reference the production form is tested against); same workspace size. */
+int isr_wgrad3x3_group_variant(const isr_wgrad_desc* descs, int32_t n, int32_t variant, void* workspace,
+                               size_t ws_bytes, isr_stream_t s);
 int isr_wgrad3x3_partials(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
 int isr_wgrad3x3_reduce(const isr_wgrad_desc* d, void* workspace, size_t ws_bytes, isr_stream_t s);
-/* Tuning: the same computation by an explicit kernel variant (0 = production;
- * 1..4 = stage-geometry alternatives, see wgrad3x3.hip), with its own workspace size. */
+/* The same computation by an explicit kernel variant, with its own workspace size: 0 = production
+ * (isr_wgrad3x3), 16 = the production tiles and split counts with compiler-visible LDS reads (the
+ * bit-identical reference of the asm-read forms); 1..15 = earlier tile forms, in tuning builds only
+ * (-DISR_TUNING; a production library returns ISR_ERR_UNSUPPORTED / 0 bytes for them). */
 size_t isr_wgrad3x3_variant_workspace_bytes(const isr_wgrad_desc* d, int32_t variant);
 int isr_wgrad3x3_variant(const isr_wgrad_desc* d, int32_t variant, void* workspace, size_t ws_bytes, isr_stream_t s);
 

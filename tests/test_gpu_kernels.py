@@ -399,34 +399,101 @@ def test_wgrad3x3_group_rdb_vs_autograd(n, h, w):
     assert lib.isr_wgrad3x3_group_workspace_bytes(arr2, 5) == 0
 
 
-@pytest.mark.parametrize("cin,cout,variant", [(64, 32, 5), (128, 32, 5), (96, 32, 2), (192, 64, 12),
-                                              (128, 128, 14), (128, 256, 14)])
-def test_wgrad3x3_row_sweep_and_asm_reads_bitwise(cin, cout, variant):
-    """Round 5: the production forms (row sweep WG::RS for 8-row 32x32 tiles; asm transposing reads
-    WG::AR for the kernel-row forms) against the round-4 form of the same tile and split count
-    (isr_wgrad3x3_variant): the same MFMAs on the same operands in the same order, so dW / db are
-    bit-identical."""
+# every production form of the weight gradient (wgrad3x3.hip pick_default<1>) — ha is always a
+# multiple of ISR_TILE_H = 32 (the ABI validates it), so the 4- and 2-row fallbacks of that pick
+# are unreachable; `kind`: plain, g_sub2 (the Scaler: gradient read through PixelShuffle(2)),
+# x_sub2 taps=1 (the discriminator's stride-2 convs on the phase decomposition)
+WGRAD_FORMS = [
+    (64, 32, "plain"),     # row sweep WG::RS (8-row stages, 2 waves per kernel column)
+    (128, 32, "plain"),    # row sweep
+    (64, 64, "plain"),     # row sweep, two cout tiles
+    (96, 32, "plain"),     # cin % 64 == 32: 4-row stages, asm reads (WG::AR)
+    (160, 32, "plain"),    # the same form at cin 160
+    (192, 64, "plain"),    # RDB final conv: 64 x 96 ci-split tile, asm reads without read-ahead (AR 2)
+    (128, 128, "plain"),   # discriminator wide form, 128 ci per block
+    (128, 256, "plain"),   # the same, two 128-cout tiles
+    (64, 128, "plain"),    # discriminator wide form, 64 ci per block
+    (64, 256, "g_sub2"),   # Scaler weight gradient (row sweep on the PixelShuffle'd gradient)
+    (256, 64, "x_sub2"),   # stride-2 phase conv, wide taps=1 form
+    (256, 32, "x_sub2"),   # stride-2 phase conv, 32-cout taps=1 form (4 waves)
+]
+
+
+@pytest.mark.parametrize("cin,cout,kind", WGRAD_FORMS)
+def test_wgrad3x3_asm_read_forms_bitwise(cin, cout, kind):
+    """The production forms read LDS through inline asm with hand-counted lgkmcnt waits (row sweep
+    WG::RS, asm-read kernel-row forms WG::AR); variant 16 runs the same tiles, split counts and MFMA
+    order with compiler-visible LDS reads.  dW / db must be bit-identical — a fragment read before
+    its wait, a compiler copy of an asm destination or an SMEM load under a counted wait would show
+    here as a difference (the static side is tools/check_lds_waits.py in the build)."""
     import ctypes
     from image_super_resolution_amd import _lib, ops
     lib = _lib.load()
     n, h, w = 2, 40, 72
-    xb = ops.ActBuffer.from_nchw(bf(_mk(n, cin, h, w, 91)), pad=1)
-    gb = ops.ActBuffer.from_nchw(bf(_mk(n, cout, h, w, 92)), pad=1)
+    if kind == "plain":
+        xb = ops.ActBuffer.from_nchw(bf(_mk(n, cin, h, w, 91)), pad=1)
+        gb = ops.ActBuffer.from_nchw(bf(_mk(n, cout, h, w, 92)), pad=1)
+        kw = {}
+    elif kind == "g_sub2":  # x at LR, the gradient of the 64-channel PixelShuffle output at 2x
+        xb = ops.ActBuffer.from_nchw(bf(_mk(n, cin, h, w, 91)), pad=1)
+        gb = ops.ActBuffer.alloc(n, 2 * h, 2 * w, cout // 4, 2, DEV, ha=2 * xb.ha, wa=2 * xb.wa)
+        gb.set_nchw(bf(_mk(n, cout // 4, 2 * h, 2 * w, 92)), 0)
+        kw = dict(g_sub2=True)
+    else:  # x at 2x with cin / 4 channels, read as PixelUnshuffle(2); the gradient at LR
+        gb = ops.ActBuffer.from_nchw(bf(_mk(n, cout, h, w, 92)), pad=1)
+        xb = ops.ActBuffer.alloc(n, 2 * h, 2 * w, cin // 4, 1, DEV, ha=2 * gb.ha, wa=2 * gb.wa)
+        xb.set_nchw(bf(_mk(n, cin // 4, 2 * h, 2 * w, 91)), 0)
+        kw = dict(x_sub2=True, taps=1)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = []
-    for v in (0, variant):
+    for v in (0, 16):
         dw = torch.full((cout, cin, 3, 3), float("nan"), device=DEV)
-        db = torch.full((cout,), float("nan"), device=DEV)
-        d = ops.wgrad3x3_desc(xb, cin, gb, cout, dw, db, scale=0.25)
+        db = None if kind == "x_sub2" else torch.full((cout,), float("nan"), device=DEV)
+        d = ops.wgrad3x3_desc(xb, cin, gb, cout, dw, db, scale=0.25, **kw)
         nb = lib.isr_wgrad3x3_variant_workspace_bytes(ctypes.byref(d), v)
         assert nb > 0
         ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
         assert lib.isr_wgrad3x3_variant(ctypes.byref(d), v, ws.data_ptr(), nb, st) == 0
         torch.cuda.synchronize()
         res.append((dw, db))
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
-    rw, rb = _wgrad_ref(xb.to_nchw(0, cin), gb.to_nchw(0, cout), 0.25)
-    _close_rel(res[0][0], rw, 1e-3)
+    taps = slice(0, 2) if kind == "x_sub2" else slice(0, 3)
+    assert torch.isfinite(res[0][0][..., taps, taps]).all()
+    assert torch.equal(res[0][0][..., taps, taps], res[1][0][..., taps, taps])
+    if res[0][1] is not None:
+        assert torch.equal(res[0][1], res[1][1])
+    if kind == "plain":
+        rw, _ = _wgrad_ref(xb.to_nchw(0, cin), gb.to_nchw(0, cout), 0.25)
+        _close_rel(res[0][0], rw, 1e-3)
+    # the round-1..4 tile forms are tuning-build only: a production library refuses them
+    if "tuning" not in os.environ.get("ISR_LIB", ""):
+        d = ops.wgrad3x3_desc(xb, cin, gb, cout, res[0][0], res[0][1], **kw)
+        assert lib.isr_wgrad3x3_variant_workspace_bytes(ctypes.byref(d), 5) == 0
+
+
+def test_wgrad3x3_group_asm_reads_bitwise():
+    """The grouped RDB launch (row sweep, asm reads) against its compiler-read form of the same
+    tiles and splits (isr_wgrad3x3_group_variant 1): bit-identical, on a 4x-cfg3-shaped RDB."""
+    import ctypes
+    from image_super_resolution_amd import _lib, ops
+    lib = _lib.load()
+    n, h, w = 2, 40, 72
+    Db = ops.ActBuffer.from_nchw(bf(_mk(n, 192, h, w, 81)), pad=1)
+    Eb = ops.ActBuffer.from_nchw(bf(_mk(n, 192, h, w, 82)), pad=1)
+    shapes = [(192, 64, 0, 0.04), (160, 32, 64, 1.0), (128, 32, 96, 1.0), (96, 32, 128, 1.0), (64, 32, 160, 1.0)]
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    res = []
+    for v in (0, 1):
+        outs = [(torch.full((co, ci, 3, 3), float("nan"), device=DEV), torch.full((co,), float("nan"), device=DEV))
+                for ci, co, _, _ in shapes]
+        arr = (_lib.IsrWgradDesc * 5)(*[ops.wgrad3x3_desc(Db, ci, Eb, co, dw, db, g_coff=gco, scale=sc)
+                                         for (ci, co, gco, sc), (dw, db) in zip(shapes, outs)])
+        nbytes = lib.isr_wgrad3x3_group_workspace_bytes(arr, 5)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+        assert lib.isr_wgrad3x3_group_variant(arr, 5, v, ws.data_ptr(), nbytes, st) == 0
+        torch.cuda.synchronize()
+        res.append(outs)
+    for (a, b), (c, d) in zip(res[0], res[1]):
+        assert torch.isfinite(a).all() and torch.equal(a, c) and torch.equal(b, d)
 
 
 def test_wgrad3x3_partials_then_reduce_equals_one_call():
