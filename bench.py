@@ -47,8 +47,10 @@ graph (engine.GraphedPlan; --no-graph for the eager ctypes launch loop, whose
   train         — BASELINE.json configs[2] per GPU: the SRGAN-mode train.py step
                   (EResNet(16) x4, VGG19 5_4 L1 + adversarial, D step, Adam/clip/EMA),
                   16 x 512² per GPU; at N > 1 with the bucketed RCCL gradient
-                  all-reduce, plus the same step without it in the same job
-                  (scaling_eff = its time / the data-parallel time).
+                  all-reduce, plus the same step without it in the same job, once on
+                  every rank at once (scaling_eff = its time / the data-parallel time)
+                  and once on rank 0 with the other ranks idle (ms_per_step_1gpu_alone,
+                  scaling_x_vs_alone: the north star's "x at 8 GPUs vs one GPU").
 """
 from __future__ import annotations
 
@@ -89,7 +91,7 @@ def parse():
                     help="tiles the CPU baseline runs one by one (the first is the warm-up; all of them are the "
                          "parity reference)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r05")
+    ap.add_argument("--round", default="r05")  # PMC traffic file (profiles/<round>_pmc_traffic.json)
     ap.add_argument("--weights", default=str(ROOT / "tests" / "golden" / "trained_resnet_x4.safetensors"),
                     help="generator state_dict (default: the committed trained ResNet(16, 0.2, x4)); "
                          "'synth' = the seeded synthetic weights of earlier rounds")
@@ -233,8 +235,31 @@ def train_leg(args, dev, world: int, rank: int) -> dict:
             dt = tt.item()
         return dt * 1e3 / steps
 
+    def run_alone(steps: int) -> float:
+        """The 1-GPU step with no peer running: rank 0 times the all-reduce-free
+        step while every other rank waits idle on the rendezvous store (a blocking socket read, no
+        spinning host thread), so the host CPUs the job shares are rank 0's alone."""
+        enable_grad_allreduce(gen, None)
+        store = dist.distributed_c10d._get_default_store()
+        key = f"isr_bench_alone_{steps}"
+        dist.barrier()
+        dt = 0.0
+        if rank == 0:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            trainer.train_srgan(gen, ema, dis, batches, tf, gl, og, od, sc, (sg, sdl), 0, None, mean=mean, std=std,
+                                steps=steps, log_every=10 ** 9, dist_group=None)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            store.set(key, "1")
+        else:
+            store.wait([key])
+        dist.barrier()
+        return dt * 1e3 / steps
+
     run(args.train_warmup, world > 1)
     ms_local = run(args.train_steps, False) if world > 1 else None
+    ms_alone = run_alone(args.train_steps) if world > 1 else None
     ms = run(args.train_steps, world > 1)
     flops = train_step_flops(batch, hr, blocks)
     res = {"workload": f"SRGAN(EResNet({blocks}, 0.2), x4) train step: VGG19 conv5_4 L1 + 1e-3 adversarial, "
@@ -250,9 +275,18 @@ def train_leg(args, dev, world: int, rank: int) -> dict:
                                            "all-reduce overlapped with the HIP backward)" if world > 1 else ""),
            "dtype": "bf16 storage, fp32 accumulation and master weights"}
     if world > 1:
+        # two 1-GPU denominators: every rank running the all-reduce-free step at once (host CPUs
+        # shared by all N processes) and rank 0 running it with the other ranks idle
         res["ms_per_step_no_allreduce"] = round(ms_local, 3)
+        res["ms_per_step_1gpu_alone"] = round(ms_alone, 3)
         res["scaling_eff"] = round(ms_local / ms, 4)
         res["scaling_x"] = round(world * ms_local / ms, 3)
+        res["scaling_eff_vs_alone"] = round(ms_alone / ms, 4)
+        res["scaling_x_vs_alone"] = round(world * ms_alone / ms, 3)
+        cores = cpu_cores()
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        res["host_cpus"] = cores["use"]
+        res["host_cpus_per_rank"] = round(cores["use"] / max(1, local_world), 2)
     del gen, dis, gl, og, od, ema
     torch.cuda.empty_cache()
     return res

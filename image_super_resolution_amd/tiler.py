@@ -88,7 +88,8 @@ def shard_tiles(tiles: Sequence[Tile], world: int) -> list[list[Tile]]:
     return out
 
 
-def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | None = None) -> list[list[Tile]]:
+def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | None = None,
+               mem_limit: int | None = None, n_scalers: int = 2) -> list[list[Tile]]:
     """Multi-GPU deal of a still as horizontal bands: the image
     splits into `world` x k full-width bands of equal core height (the last one ragged), each
     extended by `halo` LR rows above and below (clipped to the image, like a window's halo);
@@ -99,11 +100,17 @@ def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | N
     input further into the image instead (more context than the halo asks, never less), so a
     rank builds ONE plan for all its bands and runs each as one batch-1 forward over the full
     width — instead of the 3-4 window shapes at batch 1-2 an LPT deal of rs.py windows gives
-    it, and with no vertical seams.  Returns per-rank Tile lists (Tile.x = 0, Tile.w = width)."""
+    it, and with no vertical seams.  `mem_limit` (bytes) also bounds a band so that one batch-1
+    forward over it (forward_bytes) fits the device memory the caller has.  Returns per-rank Tile
+    lists (Tile.x = 0, Tile.w = width)."""
     if world < 1 or halo < 0 or height < 1 or width < 1:
         raise ValueError("plan_bands: world >= 1, halo >= 0 and a non-empty image required")
     if max_rows is None:
         max_rows = band_max_rows(width)
+    if mem_limit is not None:
+        from .ops import TILE_H
+        while max_rows > TILE_H and forward_bytes(1, max_rows, width, n_scalers) > mem_limit:
+            max_rows -= TILE_H
     k = 1
     while True:
         core = -(-height // (world * k))
@@ -123,14 +130,18 @@ def plan_bands(height: int, width: int, world: int, halo: int, max_rows: int | N
     return out
 
 
-def plan_blocks(height: int, width: int, world: int, halo: int, limit: int = 2 ** 31) -> list[list[Tile]]:
+def plan_blocks(height: int, width: int, world: int, halo: int, limit: int = 2 ** 31,
+                mem_limit: int | None = None, n_scalers: int = 2) -> list[list[Tile]]:
     """Multi-GPU deal of a still as a 2-D grid of blocks: gr x gc = world x k
     blocks of equal core (split evenly: cores differ by at most one pixel), each extended by `halo` LR pixels on every
     side and clipped at the image edge (a true image edge is the network's own zero padding, so
     clipping loses no context the whole-image forward has); rank r takes blocks [r k, (r + 1) k)
     in raster order.  k is the smallest count whose blocks fit the trunk kernel's 2 GiB window per
     16-channel plane (any still up to ~8K x 8K LR fits whole: k = 1); among the grids of that count the one with the least work on the busiest rank wins
-    (work = the blocks' tile-aligned LR area, what the trunk kernel computes).  Full-width bands
+    (work = the blocks' tile-aligned LR area, what the trunk kernel computes); with `mem_limit`
+    (bytes) a block must also fit one batch-1 forward in that much device memory (forward_bytes:
+    ~4 KB per LR pixel at x4), so a still larger than the GPU's free memory splits into more blocks
+    instead of failing to allocate.  Full-width bands
     are the gc = 1 member of this family; at cfg4 over 8 ranks the 2 x 4 grid puts 1.14 M LR px
     on the busiest rank against 1.29 M for the 334-row bands (halo 32: 8 % vs 24 % overhead).
     Returns per-rank Tile lists (raster order inside a rank)."""
@@ -151,6 +162,8 @@ def plan_blocks(height: int, width: int, world: int, halo: int, limit: int = 2 *
 
     def fits(t: Tile) -> bool:
         h, w = t.in_shape
+        if mem_limit is not None and forward_bytes(1, h, w, n_scalers) > mem_limit:
+            return False
         return 16 * 2 * (round_up(h, TILE_H) + 2) * (round_up(w, TILE_W) + 2) < limit
 
     k = 1
@@ -202,6 +215,25 @@ def plan_bytes(n: int, h: int, w: int, n_scalers: int) -> int:
         p = 4 if s == n_scalers - 1 else 1
         b += 64 * (ha + 2 * p) * (wa + 2 * p) * 2
     return n * b
+
+
+def forward_bytes(n: int, h: int, w: int, n_scalers: int) -> int:
+    """Device bytes one forward of an n x h x w uint8 batch needs: the plan's activation buffers
+    (plan_bytes), the uint8 input and output, and the 8 MB-aligned slack of torch's allocator
+    per buffer (about 4 KB per LR pixel at x4: cfg4's whole 2160 x 3840 still ~31 GiB)."""
+    s2 = 4 ** n_scalers
+    return plan_bytes(n, h, w, n_scalers) + n * 3 * h * w * (1 + s2) + 16 * (8 << 20)
+
+
+def device_budget(device, reserve: float = 0.1) -> int | None:
+    """Bytes a new forward may allocate on `device`: the device's free memory plus what torch's
+    caching allocator holds unused, less `reserve` of the total (None off the GPU)."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return None
+    free, total = torch.cuda.mem_get_info(device)
+    cached = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+    return max(0, int(free + cached - reserve * total))
 
 
 class GeneratorRunner:
@@ -275,7 +307,7 @@ class TileUpscaler:
     """
 
     def __init__(self, runner: BatchRunner, scale: int, window: int = 96, halo: int = 0, batch: int = 8,
-                 device="cuda", shard: str = "windows", gather: str = "device"):
+                 device="cuda", shard: str = "windows", gather: str = "device", mem_budget: int | None = None):
         """`shard`: "windows" runs rs.py's windows (dealt longest-processing-time-first over
         ranks, shard_tiles; the canvas equals the single-rank one bit for bit); "bands" runs
         full-width horizontal bands with the same halo (plan_bands: one rank's share is one or a
@@ -288,7 +320,11 @@ class TileUpscaler:
         point; "host" has every rank copy its tiles (device → pinned host) into one shared host canvas
         (a file in /dev/shm, all ranks on one node) that rank 0 returns as a CPU tensor — the
         still's output is written from host memory anyway (rs.py: cv2.imwrite), and the ranks' D2H
-        copies run in parallel over their own links instead of one after another into rank 0."""
+        copies run in parallel over their own links instead of one after another into rank 0.
+        `mem_budget` (bytes; default: the device's free memory when the image arrives, device_budget)
+        bounds every forward: bands / blocks are sized so that one fits, and a shape's `batch` is cut
+        to as many tiles as fit together (forward_bytes) — ADVICE r5: the 2 GiB plane window alone
+        would allow a ~250 GiB forward."""
         if batch < 1:
             raise ValueError("batch must be >= 1")
         if shard not in ("windows", "bands", "blocks"):
@@ -301,13 +337,18 @@ class TileUpscaler:
         self.device = torch.device(device)
         self.shard = shard
         self.gather = gather
+        self.mem_budget = mem_budget
+        self.n_scalers = max(0, int(scale).bit_length() - 1)
+
+    def _budget(self) -> int | None:
+        return self.mem_budget if self.mem_budget is not None else device_budget(self.device)
 
     def shards(self, height: int, width: int, world: int) -> list[list[Tile]]:
         """The per-rank tile lists of an image (deterministic: every rank computes the same)."""
         if self.shard == "bands":
-            return plan_bands(height, width, world, self.halo)
+            return plan_bands(height, width, world, self.halo, mem_limit=self._budget(), n_scalers=self.n_scalers)
         if self.shard == "blocks":
-            return plan_blocks(height, width, world, self.halo)
+            return plan_blocks(height, width, world, self.halo, mem_limit=self._budget(), n_scalers=self.n_scalers)
         tiles = plan_tiles(height, width, self.window, self.halo)
         return shard_tiles(tiles, world) if world > 1 else [tiles]
 
@@ -319,8 +360,12 @@ class TileUpscaler:
         for t in tiles:
             groups[t.in_shape].append(t)
         out: dict[int, torch.Tensor] = {}
-        step = self.batch  # windows, bands and blocks of one input shape share a batched forward
+        budget = self._budget()
         for (h, w), lst in groups.items():
+            # windows, bands and blocks of one input shape share a batched forward, as many as fit
+            step = self.batch
+            if budget is not None:
+                step = max(1, min(step, budget // max(1, forward_bytes(1, h, w, self.n_scalers))))
             for i in range(0, len(lst), step):
                 chunk = lst[i:i + step]
                 x = torch.stack([image[:, t.y0:t.y1, t.x0:t.x1] for t in chunk])

@@ -797,27 +797,42 @@ def _grad_group(gen: nn.Module):
     return gen.__dict__.get("_isr_grad_group")
 
 
+def _plan_device(plan) -> torch.device:
+    chain = getattr(plan, "chain", None)
+    return chain.state.device if chain is not None else plan.device
+
+
 def verify_chains(gen: nn.Module) -> None:
     """Blocking persistent-chain give-up check of every training forward queued so far on this
     generator (engine.ChainFailed); the trainer calls it at the end of every epoch, before the
     epoch's results (losses, checkpoint) are handed out.  Data parallel: every rank raises when
     any rank's trunk gave up (one all-reduce of the local verdict), so no rank walks on into a
-    collective its failed peer will never join."""
+    collective its failed peer will never join.  Every generator rank takes part in that
+    all-reduce, also one whose trunk fell back to per-conv launches (it votes 0) and one whose
+    check itself failed with another error (it votes 1 and re-raises that error after the
+    collective), so a peer never waits in it alone."""
     from .engine import ChainFailed
-    chain = getattr(_plan_of(gen), "chain", None)  # the Denoise training plan has no trunk chain
-    if chain is None:
+    plan = _plan_of(gen)
+    if plan is None or not hasattr(plan, "chain"):  # no training forward yet / the Denoise plan (no trunk)
         return
+    chain = plan.chain
     group = _grad_group(gen)
     if group is None:
-        chain.verify()
+        if chain is not None:
+            chain.verify()
         return
+    err, bad = None, 0
     try:
-        chain.verify()
-        bad = 0
+        if chain is not None:
+            chain.verify()
     except ChainFailed:
         bad = 1
-    t = torch.tensor([bad], dtype=torch.int32, device=chain.state.device)
+    except BaseException as e:  # noqa: BLE001 - re-raised below, after the peers have the vote
+        err, bad = e, 1
+    t = torch.tensor([bad], dtype=torch.int32, device=_plan_device(plan))
     all_reduce_(t, None if group is True else group)
+    if err is not None:
+        raise err
     if int(t.item()):
         raise ChainFailed(f"conv chain: a dependency wait gave up on {int(t.item())} rank(s); the "
                           "affected steps were skipped on every rank")
@@ -833,18 +848,22 @@ def step_guard_ptr(gen: nn.Module):
     (state[2] != state[3]) is summed over the group on the device and written into a two-word
     guard [sum, 0] that every rank's guarded Adam / EMA kernels read — all ranks skip the step
     together and the replicas stay identical.  Called once per step on every rank (one small
-    all-reduce, no host synchronisation with RCCL)."""
+    all-reduce, no host synchronisation with RCCL); a rank whose trunk ran per conv contributes 0
+    and still reads the global guard, so ranks never disagree on whether the collective runs."""
     plan = _plan_of(gen)
-    chain = getattr(plan, "chain", None)
-    if chain is None:
+    if plan is None or not hasattr(plan, "chain"):
         return None
+    chain = plan.chain
     group = _grad_group(gen)
     if group is None:
-        return chain.guard_ptr
+        return chain.guard_ptr if chain is not None else None
     g = plan.__dict__.get("_global_guard")
     if g is None:
-        g = plan.__dict__["_global_guard"] = torch.zeros(2, dtype=torch.int32, device=chain.state.device)
-    flag = (chain.state[2:3] != chain.state[3:4]).to(torch.int32)
+        g = plan.__dict__["_global_guard"] = torch.zeros(2, dtype=torch.int32, device=_plan_device(plan))
+    if chain is not None:
+        flag = (chain.state[2:3] != chain.state[3:4]).to(torch.int32)
+    else:
+        flag = torch.zeros(1, dtype=torch.int32, device=_plan_device(plan))
     all_reduce_(flag, None if group is True else group)
     g[0:1].copy_(flag)
     return g.data_ptr()

@@ -3,6 +3,7 @@ averaging used by train.py (train_engine.allreduce_grads) — same math as DDP."
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -81,7 +82,7 @@ def test_allreduce_mean_flat_bucket():
         torch.testing.assert_close(c, torch.tensor([0.5]))
 
 
-def _guard_worker(rank, world, port, q):
+def _guard_worker(rank, world, port, q, variant="chain"):
     """A trunk give-up on rank 1 only: the step guard every rank's optimiser reads must say
     "skip" on both ranks, and the epoch-end check must raise on both (the gradients
     are averaged before the guard is read, so a per-rank guard lets peers apply poisoned ones)."""
@@ -103,8 +104,14 @@ def _guard_worker(rank, world, port, q):
                 raise ChainFailed("gave up")
 
         chain = types.SimpleNamespace(state=state, guard_ptr=state.data_ptr() + 8, verify=verify)
+        if rank == 0 and variant == "fallback":  # rank 0's trunk ran per conv: no chain, still votes
+            chain = None
+        if rank == 0 and variant == "error":  # rank 0's check fails with another error: votes bad, re-raises
+            def broken():
+                raise RuntimeError("HIP error in the chain check")
+            chain.verify = broken
         gen = torch.nn.Linear(2, 2)
-        gen.__dict__["_isr_train_plan"] = types.SimpleNamespace(chain=chain)
+        gen.__dict__["_isr_train_plan"] = types.SimpleNamespace(chain=chain, device=torch.device("cpu"))
         enable_grad_allreduce(gen, True)
         ptr = step_guard_ptr(gen)
         g = gen.__dict__["_isr_train_plan"]._global_guard
@@ -115,6 +122,8 @@ def _guard_worker(rank, world, port, q):
             verify_chains(gen)
         except ChainFailed:
             raised = True
+        except RuntimeError as e:
+            raised = "other: " + str(e)
         # after the report, the accepted count caught up: the next step's guard lets updates run
         ptr2 = step_guard_ptr(gen)
         q.put((rank, words, raised, g.tolist()))
@@ -122,11 +131,15 @@ def _guard_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_trunk_give_up_guard_is_global_under_data_parallel():
+@pytest.mark.parametrize("variant", ["chain", "fallback", "error"])
+def test_trunk_give_up_guard_is_global_under_data_parallel(variant):
+    """variant 'fallback': rank 0 built no persistent chain (per-conv trunk) — it still joins both
+    collectives; 'error': rank 0's chain check raises another error — it votes 'bad', its peer
+    raises ChainFailed, rank 0 re-raises its own error, and neither blocks."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_guard_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_guard_worker, args=(r, 2, port, q, variant)) for r in range(2)]
     for p in ps:
         p.start()
     res = {r: (w, raised, w2) for r, w, raised, w2 in (q.get(timeout=120) for _ in range(2))}
@@ -136,5 +149,8 @@ def test_trunk_give_up_guard_is_global_under_data_parallel():
     for r in (0, 1):
         words, raised, after = res[r]
         assert words[0] != words[1], f"rank {r}: the guard must skip the step (words {words})"
-        assert raised, f"rank {r}: the epoch-end check must raise on every rank"
+        if variant == "error" and r == 0:
+            assert raised == "other: HIP error in the chain check", raised
+        else:
+            assert raised is True, f"rank {r}: the epoch-end check must raise ChainFailed on every rank ({raised})"
         assert after[0] == after[1], f"rank {r}: once reported, later steps update again ({after})"

@@ -151,6 +151,36 @@ def test_blocks_single_rank_equals_whole_image_host_gather():
     assert torch.equal(up(img), full)
 
 
+def test_plan_memory_bound_cfg4():
+    """blocks / bands are sized by the device memory one forward needs, not only by the
+    trunk kernel's 2 GiB plane window (which lets the whole 4K still through as one ~31 GiB forward)."""
+    whole = tiler.forward_bytes(1, 2160, 3840, 2)
+    assert 30 << 30 < whole < 34 << 30  # the measured cfg4 peak is 31.5 GiB
+    assert len(tiler.plan_blocks(2160, 3840, 1, 32)[0]) == 1
+    limit = 12 << 30
+    blocks = tiler.plan_blocks(2160, 3840, 1, 32, mem_limit=limit, n_scalers=2)[0]
+    assert len(blocks) > 1 and all(tiler.forward_bytes(1, *t.in_shape, 2) <= limit for t in blocks)
+    bands = tiler.plan_bands(2160, 3840, 1, 32, mem_limit=limit, n_scalers=2)[0]
+    assert len(bands) > 1 and all(tiler.forward_bytes(1, *t.in_shape, 2) <= limit for t in bands)
+    covered = sorted((t.y, t.h) for t in bands)
+    assert covered[0][0] == 0 and sum(h for _, h in covered) == 2160
+
+
+def test_batch_capped_by_memory_budget():
+    """run_tiles puts no more tiles of one shape into a forward than fit the budget."""
+    seen = []
+
+    def rec(x):
+        seen.append(x.shape[0])
+        return box_up(x)
+
+    budget = 2 * tiler.forward_bytes(1, 16, 16, 2) + 1
+    up = tiler.TileUpscaler(rec, S, window=16, halo=0, batch=8, device="cpu", mem_budget=budget)
+    img = image(64, 64, seed=5)
+    assert torch.equal(up(img), tiler.TileUpscaler(box_up, S, window=16, halo=0, batch=1, device="cpu")(img))
+    assert max(seen) == 2 and sum(seen) == 16
+
+
 def test_runner_shape_check():
     up = tiler.TileUpscaler(lambda x: x, S, window=8, device="cpu")
     with pytest.raises(RuntimeError, match="runner returned"):
