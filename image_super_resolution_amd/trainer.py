@@ -132,9 +132,15 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
     dsr_side = hr_overlap and os.environ.get("ISR_TRAIN_DSR_SIDE", "1") == "1"
     hr_early = hr_overlap and os.environ.get("ISR_TRAIN_HR_EARLY", "1") == "1"
     d_stream = torch.cuda.Stream(device) if overlap and device.type == "cuda" else None
+    # test-only: the generator's clip / Adam / EMA enqueued before the discriminator step instead
+    # of after it (a legal order: the two touch disjoint state; tests/test_gpu_dist_train.py)
+    g_first = os.environ.get("ISR_TRAIN_G_FIRST", "0") == "1"
     for idx in range(total):
         hr_images, lr_images = transform(next(it))
         sr_images = gen_net(lr_images)
+        _tap("sr", [sr_images])
+        if TAPS is not None and sr_images.requires_grad:  # the generator's upstream gradient (tests)
+            sr_images.register_hook(lambda g: _tap("sr_grad", [g]))
         sr_images = (sr_images + 1.0) / 2.0
         sr_images = (sr_images - mean) / std
         hr_features = None
@@ -163,12 +169,14 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
         else:
             perceptual_loss, adversarial_loss_, content_loss = compute_loss.calc_contentLoss(sr_images, hr_images,
                                                                                              sr_discriminated)
+        _tap("g_loss", [perceptual_loss, adversarial_loss_, content_loss])
         optimizer_g.zero_grad(set_to_none=True)
         if d_stream is not None:
             fwd_done = torch.cuda.Event()
             fwd_done.record()  # sr / hr and every forward the D step reads
         gradscaler_gen.scale(perceptual_loss).backward()
-        if d_stream is not None:
+        _tap("g_grad", [p.grad for p in gen_net.parameters()])
+        if d_stream is not None and not g_first:
             # the discriminator's forwards and backward on a second stream, beside the generator's
             # backward (they read neither its gradients nor anything it writes; D's weights change
             # only in D's optimiser step, after both)
@@ -178,26 +186,36 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
                                                        gradscaler_dis)
         gradscaler_gen.unscale_(optimizer_g)
         clip_grad_norm_(gen_net.parameters(), 10)
+        _tap("g_grad_clipped", [p.grad for p in gen_net.parameters()])
         guard = step_guard_ptr(_unwrap(gen_net))  # a failed trunk forward updates neither G nor D
         with step_guard(guard):
             gradscaler_gen.step(optimizer_g)
             gradscaler_gen.update()
             schedule_g.step()
             ema.update(_unwrap(gen_net))
+        _tap("g_param", list(gen_net.parameters()))
+        if d_stream is not None and g_first:  # test-only order (ISR_TRAIN_G_FIRST=1)
+            d_stream.wait_event(fwd_done)
+            with torch.cuda.stream(d_stream):
+                adversarial_loss = _d_forward_backward(dis_net, compute_loss, sr_images, hr_images, optimizer_d,
+                                                       gradscaler_dis)
 
         if d_stream is not None:
             torch.cuda.current_stream().wait_stream(d_stream)
         else:
             adversarial_loss = _d_forward_backward(dis_net, compute_loss, sr_images, hr_images, optimizer_d,
                                                    gradscaler_dis)
+        _tap("d_grad_local", [p.grad for p in dis_net.parameters()])
         if dist_group is not None:
             allreduce_grads(dis_net.parameters(), None if dist_group is True else dist_group)
+        _tap("d_grad", [p.grad for p in dis_net.parameters()])
         gradscaler_dis.unscale_(optimizer_d)
         clip_grad_norm_(dis_net.parameters(), 10)
         with step_guard(guard):
             gradscaler_dis.step(optimizer_d)
             gradscaler_dis.update()
             schedule_d.step()
+        _tap("d_param", list(dis_net.parameters()))
         pending.append(torch.stack([content_loss.detach(), adversarial_loss_.detach(), adversarial_loss.detach()]))
         if len(pending) == log_every or idx == total - 1:
             vals = torch.stack(pending).cpu().tolist()
@@ -210,6 +228,17 @@ def train_srgan(gen_net, ema: ModelEMA, dis_net, batches, transform, compute_los
             pending = []
     _verify(gen_net)
     return loss_g
+
+
+# Diagnostic taps (tests only): when TAPS is a list, train_srgan appends (name, step, [tensors])
+# with every tensor cloned on the current stream at that point of the step's enqueue order — no
+# host synchronisation, so the stream schedule being diagnosed stays as it is.
+TAPS: list | None = None
+
+
+def _tap(name: str, tensors) -> None:
+    if TAPS is not None:
+        TAPS.append((name, [None if t is None else t.detach().clone() for t in tensors]))
 
 
 def _d_frozen_forward(dis_net, sr_images):

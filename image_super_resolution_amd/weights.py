@@ -113,3 +113,28 @@ def heldout_tiles(n: int, lr_size: int = 128, scale: int = 4, seed: int = HELDOU
     lr = F.interpolate(x255, size=(lr_size, lr_size), mode="bilinear", align_corners=False, antialias=False)
     lr = (lr + 0.5).floor_().div_(255.0)
     return normalize(lr, mean, std).contiguous(), (x255 / 255.0).contiguous()
+
+
+HELDOUT_STILL_SEED = 20_261_018
+
+
+def heldout_still(h: int, w: int, scale: int, seed: int = HELDOUT_STILL_SEED, tile: int = 512, device="cuda"):
+    """A large held-out image of the trained weights' distribution: an HR mosaic of `tile`² dead-leaves
+    images (data.leaves_hr_u8 at the training crops' size, one generator per still), cropped to
+    (scale*h, scale*w), and its LR = train.py's transform (uint8 bilinear resize rounded half up,
+    heldout_tiles' formula).  Returns (LR uint8 [3, h, w], HR uint8 [3, scale*h, scale*w]) on the CPU —
+    the cfg4 still (3840x2160 -> 15360x8640) and the cfg5 frames (1920x1080 -> 3840x2160) of the
+    parity tests."""
+    import torch.nn.functional as F
+
+    from .data import leaves_hr_u8
+    th, tw = -(-scale * h // tile), -(-scale * w // tile)
+    g = torch.Generator(device=device).manual_seed(seed)
+    hr = torch.empty(3, th * tile, tw * tile, dtype=torch.uint8, device=device)
+    for i in range(th):
+        for j in range(tw):
+            hr[:, i * tile:(i + 1) * tile, j * tile:(j + 1) * tile] = leaves_hr_u8(1, tile, g, device)[0]
+    hr = hr[:, :scale * h, :scale * w].contiguous()
+    lr = F.interpolate(hr[None].float(), size=(h, w), mode="bilinear", align_corners=False, antialias=False)
+    lr = (lr + 0.5).floor_().clamp_(0, 255).to(torch.uint8)[0]
+    return lr.cpu(), hr.cpu()

@@ -10,6 +10,8 @@ fp32 with tanh.  Switches turn single rounding sites off to attribute the error:
 
     python tests/diag_precision.py --weights tests/golden/trained_resnet_x4.safetensors
     python tests/diag_precision.py --synth 5          # the synthetic weights of the older tests
+    python tests/diag_precision.py --weights tests/golden/trained_resnet_x2.safetensors --scale 2 \
+        --hip gpurun_out/r06/trained_heldout_hip_y_x2.pt
 
 Reports PSNR(emulation vs fp32 oracle), |dPSNR vs HR| per configuration, and optionally the same
 for a saved HIP output (--hip gpurun_out/.../trained_heldout_hip_y.pt) to check the emulation.
@@ -91,6 +93,7 @@ def main():
     ap.add_argument("--lr-size", type=int, default=128)
     ap.add_argument("--hip", default=None, help="saved HIP output of the first tiles (train_weights.py)")
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--scale", type=int, default=4, choices=(2, 4))
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     torch.set_grad_enabled(False)
@@ -98,15 +101,15 @@ def main():
     from image_super_resolution_amd.weights import heldout_tiles, normalize, synth_lr_batch, synth_state_dict
     if a.weights:
         sd = checkpoint.load_module_state(a.weights)
-        lr, hr = heldout_tiles(a.tiles, a.lr_size, 4)
+        lr, hr = heldout_tiles(a.tiles, a.lr_size, a.scale)
     else:
-        sd = {k: v.float() for k, v in synth_state_dict(models.ResNet(16, 0.2, scaleRate=4).state_dict(),
+        sd = {k: v.float() for k, v in synth_state_dict(models.ResNet(16, 0.2, scaleRate=a.scale).state_dict(),
                                                             a.synth or 0).items()}
-        lr01, hr = synth_lr_batch(a.tiles, a.lr_size, a.lr_size, seed=1234, scale=4)
+        lr01, hr = synth_lr_batch(a.tiles, a.lr_size, a.lr_size, seed=1234, scale=a.scale)
         lr = normalize(lr01)
     nb = R.count_blocks(sd)
     hr1 = hr * 2 - 1
-    ref = R.generator(sd, lr, num_blocks=nb, scale=4)
+    ref = R.generator(sd, lr, num_blocks=nb, scale=a.scale)
     p_ref = psnr(ref, hr1)
     print(f"oracle fp32: PSNR vs HR {p_ref:.3f} dB (MSE {4 / 10 ** (p_ref / 10):.3e})")
     if a.hip:
@@ -117,7 +120,7 @@ def main():
     cfgs = [("all sites", full)] + [(f"all but {s}", tuple(x for x in full if x != s)) for s in full] + \
            [(f"only {s}", (s,)) for s in full]
     for name, sites in cfgs:
-        e = Emu(sd, sites).forward(lr, nb, 4)
+        e = Emu(sd, sites).forward(lr, nb, a.scale)
         print(f"{name:16s}: vs oracle {psnr(e, ref):7.2f} dB   dPSNR vs HR {abs(psnr(e, hr1) - p_ref):.5f} dB",
               flush=True)
 

@@ -64,9 +64,11 @@ class _PerRankD(torch.nn.Module):
         return torch.cat([self.d(c.contiguous()) for c in x.chunk(self.parts)])
 
 
-def _worker(rank, world, port, mode, tmp, q, bucket_mb="0"):
+def _worker(rank, world, port, mode, tmp, q, bucket_mb="0", g_first=False, taps=False, steps=STEPS):
     sys.path.insert(0, str(ROOT))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    # the generator's optimiser launches before (1) or after (0, default) the discriminator step
+    os.environ["ISR_TRAIN_G_FIRST"] = "1" if g_first else "0"
     # "0": every backward segment (tail, each RRDB, head) its own all-reduce bucket, so the
     # overlapped bucket schedule (train_engine._Buckets) is exercised at this tiny depth; "8"
     # (the default size): one merged bucket holding main-stream (tail, head) AND side-stream
@@ -84,14 +86,16 @@ def _worker(rank, world, port, mode, tmp, q, bucket_mb="0"):
             dist.init_process_group("gloo", rank=rank, world_size=world)
             group = True
         args = ["--enchant", "--scale", "4", "--rs_deep", "1", "--batch_size", str(HALF), "--shape", str(SHAPE),
-                "--epochs", "1", "--lr", "1e-3", "--work_dir", tmp, "--synthetic", "--steps", str(STEPS),
+                "--epochs", "1", "--lr", "1e-3", "--work_dir", tmp, "--synthetic", "--steps", str(steps),
                 "--dist_backend", "gloo", "--save_name", f"dp{world}"]
         opt = train.parse((["--resnet"] if mode == "res" else []) + args)
         train.first_setup(opt.seed)  # as train.main: identical seeds on every rank
         if rank == 1 and mode == "res":
             torch.manual_seed(777)  # rank 1 would start elsewhere: broadcast_params must fix it
         mean, std = list(data.IMAGENET_MEAN), list(data.IMAGENET_STD)
-        batches = [b.to(dev) for b in _batches(world, rank)]
+        batches = [b.to(dev) for b in _batches(world, rank)][:steps]
+        if taps:
+            trainer.TAPS = []
         sc = torch.amp.GradScaler("cuda", enabled=False)
         out = {}
         if mode == "res":
@@ -109,10 +113,22 @@ def _worker(rank, world, port, mode, tmp, q, bucket_mb="0"):
             tf = data.GPUTransform(4, hr_norm=True, mean=mean, std=std, device=dev)
             dnet = _PerRankD(dis, 2) if world == 1 else dis
             trainer.train_srgan(gen, ema, dnet, batches, tf, loss_fn, og, od, (sc, sc), (sg, sd), 0, None,
-                                mean=mean, std=std, steps=STEPS, dist_group=group)
+                                mean=mean, std=std, steps=steps, dist_group=group)
             out["g"] = {k: v.detach().cpu().numpy().copy() for k, v in gen.named_parameters()}
             out["d"] = {k: v.detach().cpu().numpy().copy() for k, v in dis.named_parameters()}
         torch.cuda.synchronize()
+        if taps:  # tools/diag_dp_order.py: large tensors travel as a strided sample + their sum
+            def small(t):
+                if t is None:
+                    return None
+                f = t.flatten().float()
+                if f.numel() <= 1 << 20:
+                    return f.cpu().numpy()
+                return np.concatenate([f[::max(1, f.numel() >> 16)].cpu().numpy(), [f.double().sum().item()]])
+            out["taps"] = [(name, [small(t) for t in ts]) for name, ts in trainer.TAPS]
+            out["names"] = {"g": [k for k, _ in (model if mode == "res" else gen).named_parameters()],
+                            "d": [k for k, _ in dis.named_parameters()] if mode != "res" else []}
+            trainer.TAPS = None
         q.put((rank, world, out))
         if world > 1:
             dist.destroy_process_group()
@@ -122,11 +138,12 @@ def _worker(rank, world, port, mode, tmp, q, bucket_mb="0"):
         raise
 
 
-def _run(mode, world, tmp, bucket_mb="0"):
+def _run(mode, world, tmp, bucket_mb="0", g_first=False, taps=False, steps=STEPS):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, str(tmp), q, bucket_mb)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, str(tmp), q, bucket_mb, g_first, taps, steps))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = {}

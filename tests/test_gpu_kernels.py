@@ -441,7 +441,7 @@ def test_wgrad3x3_asm_read_forms_bitwise(cin, cout, kind):
         kw = dict(g_sub2=True)
     else:  # x at 2x with cin / 4 channels, read as PixelUnshuffle(2); the gradient at LR
         gb = ops.ActBuffer.from_nchw(bf(_mk(n, cout, h, w, 92)), pad=1)
-        xb = ops.ActBuffer.alloc(n, 2 * h, 2 * w, cin // 4, 1, DEV, ha=2 * gb.ha, wa=2 * gb.wa)
+        xb = ops.ActBuffer.alloc(n, 2 * h, 2 * w, cin // 4, 2, DEV, ha=2 * gb.ha, wa=2 * gb.wa)
         xb.set_nchw(bf(_mk(n, cin // 4, 2 * h, 2 * w, 91)), 0)
         kw = dict(x_sub2=True, taps=1)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

@@ -9,6 +9,9 @@ SRGAN(16, 0.2, enchant=True, 4) — the 16-RRDB EResNet x4 generator — on a ba
   the same discriminator and VGG.
 * A 2-sample slice of the batch (full 128² LR crops, the same 16 RRDBs) through a pixel-loss
   step vs autograd of the fp32 oracle (oracle/ref_cpu.generator) at the test_gpu_train.py bars.
+* train.py's DEFAULT SRGAN mode (enchant=False, train.py:304-388): the BatchNorm ResNet generator
+  inside SRGAN with the post-ReLU VGG MSE content loss (utils/loss.py:16-24), one train_srgan step
+  end to end vs the fp32 oracle.
 """
 import os
 import warnings
@@ -17,7 +20,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from image_super_resolution_amd import data, loss as L, models, optim, trainer
+from image_super_resolution_amd import checkpoint, data, loss as L, models, optim, trainer
 from image_super_resolution_amd.weights import synth_state_dict
 from oracle import ref_cpu as R
 
@@ -159,3 +162,87 @@ def test_srgan_d_overlap_same_updates(monkeypatch):
     assert l0 == l1
     assert all(torch.equal(a, b) for a, b in zip(g0, g1))
     assert all(torch.equal(a, b) for a, b in zip(d0, d1))
+
+
+def test_srgan_default_mode_step_vs_oracle():
+    """One trainer.train_srgan step of SRGAN(16, 0.2, enchant=False, x2) — train.py's default mode,
+    started as train.py starts it from the pretrained --resnet generator (the committed x2 weights):
+    BatchNorm ResNet generator (train-mode batch statistics), content loss = MSE of VGG19 conv5_4
+    AFTER its ReLU, + 1e-3 BCE adversarial — on 2 crops of 128² HR, against the fp32 oracle:
+    * the generator output (train-mode BN) vs oracle.ref_cpu.generator(train_bn=True): >= 40 dB;
+    * the logged content / adversarial losses vs the oracle's content_loss (utils/loss.py:16-24) on
+      the oracle's own SR image, the stock fp32 discriminator modules and the same VGG weights:
+      rel <= 3 % (the VGG feature bar of test_gpu_vgg.py);
+    * every generator parameter gradient of the step vs autograd of the oracle generator fed the
+      step's own upstream gradient dL/dSR (the VGG + discriminator input gradients, pinned by
+      test_gpu_vgg.py / test_gpu_disc.py): rel L2 <= 5e-2, cos >= 0.998 (test_gpu_train.py's bars)."""
+    import copy
+
+    torch.manual_seed(0)
+    # train.py's default mode starts SRGAN from the --resnet checkpoint (SRGAN.init_weight loads its
+    # EMA generator, utils/models.py:659-665): the committed trained ResNet(16, 0.2, x2)
+    gen = models.SRGAN(16, 0.2, False, 2)
+    gen.res_net.load_state_dict(checkpoint.load_module_state(
+        __import__("pathlib").Path(__file__).parent / "golden" / "trained_resnet_x2.safetensors"))
+    gen = gen.to(DEV)
+    assert isinstance(gen.res_net, models.ResNet)  # the BatchNorm generator
+    dis = models.Discriminator(3, 64, 8, 1024).to(DEV)
+    dis.use_libisr(True)
+    dis_ref = copy.deepcopy(dis).cpu().use_libisr(False).train()
+    sd_g = {k: v.detach().cpu().clone().float() for k, v in gen.res_net.state_dict().items()}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        gl = L.gen_loss(device=DEV, beforeAct=False)
+    sd_vgg = {k: v.detach().cpu().float() for k, v in gl.vgg_net.state_dict().items()}
+    mean, std = list(data.IMAGENET_MEAN), list(data.IMAGENET_STD)
+    og = optim.FusedAdam(gen.parameters(), lr=1e-4)
+    od = optim.FusedAdam(dis.parameters(), lr=1e-4)
+    sg = torch.optim.lr_scheduler.LinearLR(og, 1, 0.01, total_iters=1)
+    sdl = torch.optim.lr_scheduler.LinearLR(od, 1, 0.01, total_iters=1)
+    ema = models.ModelEMA(gen, tau=1)
+    ema.ema.to(DEV)
+    sc = (torch.amp.GradScaler("cuda", enabled=False), torch.amp.GradScaler("cuda", enabled=False))
+    tf = data.GPUTransform(2, hr_norm=True, mean=mean, std=std, device=DEV)
+    crops = next(data.SyntheticSR(2, 128, seed=7, device=DEV, kind="leaves"))
+    hr, lr = tf(crops)
+    trainer.TAPS = []
+    try:
+        trainer.train_srgan(gen, ema, dis, iter([crops]), tf, gl, og, od, sc, (sg, sdl), 0, None, mean=mean,
+                            std=std, steps=1, log_every=1)
+        torch.cuda.synchronize()
+        taps = {name: [t.cpu() if t is not None else None for t in ts] for name, ts in trainer.TAPS}
+    finally:
+        trainer.TAPS = None
+    sr_hip, gy = taps["sr"][0], taps["sr_grad"][0].float()
+    perceptual, adversarial, content = (t.float().item() for t in taps["g_loss"])
+
+    # oracle: the same generator (train-mode BN), the same loss on its own SR image
+    pnames = {k for k, _ in gen.res_net.named_parameters()}
+    params = {k: v.requires_grad_(True) for k, v in sd_g.items() if k in pnames}
+    sr_ref = R.generator(sd_g, lr.float().cpu(), num_blocks=16, scale=2, enchant=False, train_bn=True)
+    agree = R.psnr(sr_hip, sr_ref.detach())
+    m, s_ = torch.tensor(mean).view(1, 3, 1, 1), torch.tensor(std).view(1, 3, 1, 1)
+    with torch.no_grad():
+        srn = ((sr_ref.detach() + 1) / 2 - m) / s_
+        for p in dis_ref.parameters():
+            p.requires_grad_(False)
+        p_ref, a_ref, c_ref = R.content_loss(sd_vgg, srn, hr.float().cpu(), dis_ref(srn), before_act=False)
+    print(f"default SRGAN mode: SR agreement {agree:.2f} dB; content {content:.6f} vs {c_ref.item():.6f}, "
+          f"adversarial {adversarial:.5f} vs {a_ref.item():.5f}")
+    assert agree >= 40.0, agree
+    assert abs(content - c_ref.item()) <= 3e-2 * abs(c_ref.item()), (content, c_ref.item())
+    assert abs(adversarial - a_ref.item()) <= 3e-2 * abs(a_ref.item()) + 1e-3, (adversarial, a_ref.item())
+    assert abs(perceptual - (content + 1e-3 * adversarial)) <= 1e-5 * abs(perceptual) + 1e-7
+
+    # generator gradients for the step's own upstream gradient
+    sr_ref.backward(gy)
+    names = [k for k, _ in gen.named_parameters()]
+    worst = []
+    for name, g in zip(names, taps["g_grad"]):
+        r = params[name[len("res_net."):]].grad
+        rel = ((g - r).norm() / r.norm().clamp_min(1e-12)).item()
+        cos = F.cosine_similarity(g.flatten().double(), r.flatten().double(), dim=0).item()
+        worst.append((rel, cos, name))
+        assert rel <= 5e-2 and cos >= 0.998, f"{name}: rel {rel:.3e} cos {cos:.5f}"
+    worst.sort(reverse=True)
+    print("default SRGAN mode, worst generator gradients vs oracle autograd:", worst[:3])

@@ -1,16 +1,20 @@
 """Video path on the GPU (video.py): the HIP-graph-captured per-batch forward equals
-the eager plan bit for bit and the uint8 oracle (utils/models.py Model) within
-1 LSB; the streaming pipeline writes every frame, in order, incl. a ragged last batch."""
+the eager plan bit for bit and, with the committed trained ResNet(16, 0.2, x2)
+(tests/golden/trained_resnet_x2.safetensors) on dead-leaves frames of its data distribution, the
+uint8 oracle (utils/models.py Model) within the north-star bars of tests/parity_bars.py; the
+streaming pipeline writes every frame, in order, incl. a ragged last batch."""
 import numpy as np
 import pytest
 import torch
 
-from image_super_resolution_amd import models, tiler, video
-from image_super_resolution_amd.weights import synth_state_dict
+from image_super_resolution_amd import checkpoint, models, tiler, video
+from image_super_resolution_amd.weights import heldout_still, synth_state_dict
 from oracle import ref_cpu as R
+from parity_bars import float_dpsnr, u8_bars
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+WEIGHTS = __import__("pathlib").Path(__file__).parent / "golden" / "trained_resnet_x2.safetensors"
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -18,9 +22,13 @@ def lib(built_lib):
     return built_lib
 
 
-def _setup(h=24, w=40, batch=2):
-    net = models.ResNet(2, 0.2, scaleRate=2)
-    sd = synth_state_dict(net.state_dict(), 11)
+def _setup(h=24, w=40, batch=2, trained=False):
+    if trained:
+        net = models.ResNet(16, 0.2, scaleRate=2)
+        sd = {k: v.float() for k, v in checkpoint.load_module_state(WEIGHTS).items()}
+    else:  # the pipeline tests need no model quality: a 2-block net keeps them fast
+        net = models.ResNet(2, 0.2, scaleRate=2)
+        sd = synth_state_dict(net.state_dict(), 11)
     net.load_state_dict(sd)
     m = models.Model(net.eval())
     m.init_normalize((0.485, 0.456, 0.406), (0.229, 0.224, 0.225))
@@ -31,19 +39,27 @@ def _setup(h=24, w=40, batch=2):
 
 @torch.no_grad()
 def test_graph_forward_matches_eager_and_oracle():
-    sd, runner, up = _setup()
-    frames = list(video.SyntheticVideo(40, 24, 2, seed=3))
+    h, w = 96, 160
+    sd, runner, up = _setup(h, w, 2, trained=True)
+    frames, hrs = [], []
+    for i in range(2):  # two dead-leaves frames (held-out stills of the x2 weights' distribution)
+        lr, hr = heldout_still(h, w, 2, seed=31 + i, device=DEV)
+        frames.append(lr.permute(1, 2, 0).contiguous().numpy())
+        hrs.append(hr)
     x = torch.from_numpy(np.stack(frames))
     got = up(x).cpu()                                    # BGR HWC
     eager = runner(x.permute(0, 3, 1, 2).contiguous().to(DEV)).cpu()   # RGB CHW
     assert torch.equal(got, eager.flip(1).permute(0, 2, 3, 1))
-    ref = R.model_u8(sd, x.permute(0, 3, 1, 2).contiguous(), num_blocks=2, scale=2)
-    d = (eager.int() - ref.int()).abs()
-    psnr_u8 = 10 * np.log10(255.0 ** 2 / (d.float() ** 2).mean().item())
-    # bf16 path vs fp32 oracle on noisy frames: >= 99 % of pixels within 1 LSB, >= 45 dB
-    assert (d <= 1).float().mean() >= 0.99 and d.max() <= 4 and psnr_u8 >= 45.0, (d.max(), psnr_u8)
+    xin = R.normalize_u8(x.permute(0, 3, 1, 2).contiguous())
+    ref_f = R.generator(R.fuse_state_dict(sd), xin, num_blocks=16, scale=2)
+    hr = torch.stack(hrs)
+    net = models.ResNet(16, 0.2, scaleRate=2)
+    net.load_state_dict(sd)
+    yf = net.eval().to(DEV)(xin.to(DEV)).float().cpu()  # the float output the uint8 path rounds
+    float_dpsnr(yf, ref_f, hr.float() / 255.0, "video batch of 2 (96x160 -> 192x320)")
+    u8_bars(eager, R.tanh_to_u8(ref_f), hr, "video batch")
     # replaying again with other frames gives their result (static buffers re-read)
-    x2 = torch.from_numpy(np.stack(list(video.SyntheticVideo(40, 24, 2, seed=9))))
+    x2 = torch.from_numpy(np.stack(list(video.SyntheticVideo(w, h, 2, seed=9))))
     assert torch.equal(up(x2).cpu(), runner(x2.permute(0, 3, 1, 2).contiguous().to(DEV)).cpu().flip(1).permute(0, 2, 3, 1))
 
 
