@@ -2,7 +2,7 @@
 """4x RRDB super-resolution inference benchmark on MI355X (BASELINE.json configs[1]).
 
 Workload: ResNet(num_block_resnet=16, add_rate=0.2, scaleRate=4) — the reference's
-RRDB generator (utils/models.py:592-618) — bf16 on the HIP kernels, 16 synthetic
+RRDB generator (utils/models.py:592-618) — fp16 storage, fp32 accumulation on the HIP kernels, 16 synthetic
 128x128 LR tiles per GPU → 16 x 512x512 HR, inputs resident in HBM.  One step =
 one generator forward over the batch on one HIP stream: head9x9, the whole RRDB trunk as
 ONE persistent launch (isr_conv_chain → trunk.hip), conv1, two Scalers, tail9x9
@@ -481,7 +481,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp16" if gw.dtype == torch.float16 else "bf16",
             "data": f"synthetic: {weights_desc} (no COCO offline)",
             "config": {"workload": f"ResNet({args.blocks}, 0.2, scaleRate={S}) RRDB inference, "
                                    f"{hw}x{hw}->{hw * S}x{hw * S}",

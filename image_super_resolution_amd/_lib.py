@@ -29,12 +29,12 @@ class IsrConvDesc(ctypes.Structure):
                 ("wpack", c_void_p), ("bias", c_void_p),
                 ("slope", c_float), ("s1", c_float), ("s2", c_float), ("shuffle", c_int32),
                 ("m", IsrView), ("mslope", c_float), ("m_c0", c_int32), ("r1_cn", c_int32), ("x_sub2", c_int32),
-                ("taps", c_int32)]
+                ("taps", c_int32), ("f16", c_int32)]
 
 
 class IsrChainDesc(ctypes.Structure):
     _fields_ = [("layers", c_void_p), ("kinds", c_void_p), ("nl", c_int32), ("n", c_int32), ("ha", c_int32),
-                ("wa", c_int32), ("state", c_void_p), ("acquire", c_int32)]
+                ("wa", c_int32), ("state", c_void_p), ("acquire", c_int32), ("f16", c_int32)]
 
 
 class IsrHeadDesc(ctypes.Structure):
@@ -42,13 +42,13 @@ class IsrHeadDesc(ctypes.Structure):
                 ("cout", c_int32), ("x", c_void_p), ("x_u8", c_int32),
                 ("mean", c_float * 3), ("inv_std", c_float * 3),
                 ("y", IsrView), ("y2", IsrView), ("wpack", c_void_p), ("bias", c_void_p), ("slope", c_float),
-                ("m", IsrView), ("mslope", c_float)]
+                ("m", IsrView), ("mslope", c_float), ("f16", c_int32)]
 
 
 class IsrTailDesc(ctypes.Structure):
     _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32),
                 ("cin", c_int32), ("x", IsrView), ("wpack", c_void_p), ("bias", c_void_p),
-                ("y", c_void_p), ("y_u8", c_int32)]
+                ("y", c_void_p), ("y_u8", c_int32), ("f16", c_int32)]
 
 
 class IsrWgradDesc(ctypes.Structure):
@@ -78,7 +78,7 @@ class IsrSrTransformDesc(ctypes.Structure):
 class IsrConvertDesc(ctypes.Structure):
     _fields_ = [("n", c_int32), ("h", c_int32), ("w", c_int32), ("ha", c_int32), ("wa", c_int32), ("c", c_int32),
                 ("nchw", c_void_p), ("v", IsrView), ("scale", c_void_p), ("shift", c_void_p),
-                ("m", IsrView), ("mslope", c_float)]
+                ("m", IsrView), ("mslope", c_float), ("f16", c_int32)]
 
 
 class IsrPoolDesc(ctypes.Structure):
@@ -138,6 +138,9 @@ SIGNATURES = {
     "isr_pack_head9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "isr_tail9x9_packed_bytes": (c_size_t, [c_int32, c_int32]),
     "isr_pack_tail9x9": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "isr_pack_conv3x3_f16": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "isr_pack_head9x9_f16": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "isr_pack_tail9x9_f16": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "isr_conv3x3_fwd": (c_int32, [POINTER(IsrConvDesc), c_void_p]),
     "isr_conv3x3_fwd_variant": (c_int32, [POINTER(IsrConvDesc), c_int32, c_void_p]),
     "isr_tuning_conv_stamps": (c_int32, [c_void_p]),

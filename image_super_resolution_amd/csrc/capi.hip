@@ -23,13 +23,14 @@ int trunk_deep_stats(unsigned long long* out, int reset);
 int trunk_item_stamps_set(void* p);
 size_t conv3x3_packed_bytes(int cout, int cin);
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
+int conv3x3_pack_f16(const float* w, void* out, int cout, int cin, hipStream_t s);
 int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s);
 int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s);
 int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s);
 size_t head9x9_packed_bytes(int cout);
 size_t tail9x9_packed_bytes();
-int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
-int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
+int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s, bool h);
+int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s, bool h);
 int conv3x3_pack_dgrad(const float* w, void* out, int cout, int cin, float scale, int sub2, hipStream_t s);
 int conv3x3_pack_batch(const isr_pack_item* items, int n, hipStream_t s);
 int ew_combine_dispatch(const isr_ew_desc* d, hipStream_t s);
@@ -173,16 +174,36 @@ int isr_pack_conv3x3_dgrad(const float* w, void* packed, int32_t cout, int32_t c
     return launched(isr::conv3x3_pack_dgrad(w, packed, cout, cin, scale, sub2, (hipStream_t)s), "pack_conv3x3_dgrad");
 }
 
-int isr_pack_head9x9(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+static int pack_head_any(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s, bool h) {
     if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_head9x9: null pointer");
     if (cout != 64 || cin < 1 || cin > 3) return fail(ISR_ERR_UNSUPPORTED, "pack_head9x9: need cout 64, cin <= 3 (got %d, %d)", cout, cin);
-    return launched(isr::head9x9_pack(w, packed, cout, cin, (hipStream_t)s), "pack_head9x9");
+    return launched(isr::head9x9_pack(w, packed, cout, cin, (hipStream_t)s, h), "pack_head9x9");
+}
+int isr_pack_head9x9(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+    return pack_head_any(w, packed, cout, cin, s, false);
+}
+int isr_pack_head9x9_f16(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+    return pack_head_any(w, packed, cout, cin, s, true);
 }
 
-int isr_pack_tail9x9(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+static int pack_tail_any(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s, bool h) {
     if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_tail9x9: null pointer");
     if (cout != 3 || cin != 64) return fail(ISR_ERR_UNSUPPORTED, "pack_tail9x9: need cout 3, cin 64 (got %d, %d)", cout, cin);
-    return launched(isr::tail9x9_pack(w, packed, cout, cin, (hipStream_t)s), "pack_tail9x9");
+    return launched(isr::tail9x9_pack(w, packed, cout, cin, (hipStream_t)s, h), "pack_tail9x9");
+}
+int isr_pack_tail9x9(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+    return pack_tail_any(w, packed, cout, cin, s, false);
+}
+int isr_pack_tail9x9_f16(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+    return pack_tail_any(w, packed, cout, cin, s, true);
+}
+
+int isr_pack_conv3x3_f16(const float* w, void* packed, int32_t cout, int32_t cin, isr_stream_t s) {
+    if (!w || !packed) return fail(ISR_ERR_BAD_DESC, "pack_conv3x3_f16: null pointer");
+    if (cin <= 0 || cin % 16) return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3_f16: cin %d must be a positive multiple of 16", cin);
+    if (cout <= 0 || cout % 32)
+        return fail(ISR_ERR_UNSUPPORTED, "pack_conv3x3_f16: cout %d must be a positive multiple of 32", cout);
+    return launched(isr::conv3x3_pack_f16(w, packed, cout, cin, (hipStream_t)s), "pack_conv3x3_f16");
 }
 
 static int conv3x3_validate(const isr_conv_desc* d) {
@@ -228,6 +249,9 @@ static int conv3x3_validate(const isr_conv_desc* d) {
         if (d->r2.data && !view_ok(d->r2, d->ha, d->wa, 0, d->cout, "conv3x3.r2", 1)) return ISR_ERR_BAD_DESC;
     }
     if (d->bias && ((uintptr_t)d->bias % 16)) return fail(ISR_ERR_BAD_DESC, "conv3x3: bias must be 16-byte aligned");
+    if (d->f16 != 0 && d->f16 != 1) return fail(ISR_ERR_BAD_DESC, "conv3x3: f16 must be 0 or 1");
+    if (d->f16 && (d->m.data || d->x_sub2 || d->taps))
+        return fail(ISR_ERR_UNSUPPORTED, "conv3x3: fp16 activations are forward-only (no mask, x_sub2 or tap window)");
     return ISR_OK;
 }
 
@@ -250,6 +274,9 @@ int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_
         return fail(ISR_ERR_BAD_DESC, "conv chain: null layers / kinds / state or nl not in [1, 1024]");
     if (c->n <= 0 || c->ha <= 0 || c->wa <= 0 || c->ha % 16 || c->wa % 32)
         return fail(ISR_ERR_BAD_DESC, "conv chain: bad grid n=%d ha=%d wa=%d", c->n, c->ha, c->wa);
+    if (c->f16 != 0 && c->f16 != 1) return fail(ISR_ERR_BAD_DESC, "conv chain: f16 must be 0 or 1");
+    if (c->f16 && variant != 0)
+        return fail(ISR_ERR_UNSUPPORTED, "conv chain: fp16 storage runs the production trunk form (variant 0) only");
     if (variant == 0 || (variant >= 2 && variant <= 9)) {
         static const int form_of[10] = {0, 0, 1, 2, 3, 4, 5, 6, 7, 8};
         const int rc = isr::trunk_launch(c, (hipStream_t)s, form_of[variant]);
@@ -332,6 +359,8 @@ int isr_head9x9_fwd(const isr_head_desc* d, isr_stream_t s) {
     if (d->y2.data && !view_ok(d->y2, d->ha, d->wa, 0, 64, "head9x9.y2", 1)) return ISR_ERR_BAD_DESC;
     if (d->m.data && !view_ok(d->m, d->ha, d->wa, 0, 64, "head9x9.m", 1)) return ISR_ERR_BAD_DESC;
     if (d->bias && ((uintptr_t)d->bias % 16)) return fail(ISR_ERR_BAD_DESC, "head9x9: bias must be 16-byte aligned");
+    if (d->f16 != 0 && d->f16 != 1) return fail(ISR_ERR_BAD_DESC, "head9x9: f16 must be 0 or 1");
+    if (d->f16 && d->m.data) return fail(ISR_ERR_UNSUPPORTED, "head9x9: fp16 activations are forward-only (no mask)");
     return launched(isr::head9x9_fwd_dispatch(d, (hipStream_t)s), "head9x9");
 }
 
@@ -343,6 +372,7 @@ static int tail_validate(const isr_tail_desc* d) {
     if (d->cin != 64) return fail(ISR_ERR_UNSUPPORTED, "tail9x9: cin must be 64");
     if (!d->y || !d->wpack) return fail(ISR_ERR_BAD_DESC, "tail9x9: null output or weights");
     if (!view_ok(d->x, d->ha, d->wa, 4, 64, "tail9x9.x", 1)) return ISR_ERR_BAD_DESC;
+    if (d->f16 != 0 && d->f16 != 1) return fail(ISR_ERR_BAD_DESC, "tail9x9: f16 must be 0 or 1");
     return ISR_OK;
 }
 

@@ -54,9 +54,11 @@ __device__ __forceinline__ void conv_stamp(int slot, int row = -1) {
 }
 
 template <int R_, int WM_, int NF_, int KC_, int NST_, int CIN_ = 0, int ABL_ = 0, int PIPE_ = (NF_ == 1), int EPQ_ = 4,
-          int SPL_ = 0, int TWN_ = 0, int NSW_ = 0, int FOLD_ = 0>
+          int SPL_ = 0, int TWN_ = 0, int NSW_ = 0, int FOLD_ = 0, int H_ = 0>
 struct C3 {
     static constexpr int R = R_, WM = WM_, NF = NF_, KC = KC_, NST = NST_;
+    // storage type of activations and weights: 0 = bf16, 1 = fp16 (isr_conv_desc.f16, inference)
+    static constexpr bool H = H_ != 0;
     // 1: the RDB residual fold (r1 == the conv's own input channels, see fold_ok) is compiled in;
     // only the RDB final-conv instantiations carry it (it costs registers)
     static constexpr int FOLD = FOLD_;
@@ -122,9 +124,9 @@ template <int V> struct IC { static constexpr int value = V; };
 
 // A operand of the residual fold: (1/s1) I on couts [16 h16, 16 h16 + 16) of a 32-cout
 // fragment (lane l supplies A[l & 31][8 (l >> 5) .. + 8]); trunk.hip builds the same.
-__device__ __forceinline__ uint32_t fold_idv(float s1) {  // bf16 bits of 1/s1, in an SGPR
-    const __bf16 bi = (__bf16)(1.f / s1);
-    return __builtin_amdgcn_readfirstlane((uint32_t)__builtin_bit_cast(uint16_t, bi));
+template <bool H>
+__device__ __forceinline__ uint32_t fold_idv(float s1) {  // storage-type bits of 1/s1, in an SGPR
+    return __builtin_amdgcn_readfirstlane((uint32_t)bits16<H>(1.f / s1));
 }
 __device__ __forceinline__ bf16x8 fold_a(uint32_t idv, int h16) {
     int lane = threadIdx.x & 63;
@@ -149,7 +151,8 @@ __device__ __forceinline__ bool fold_ok(const Desc& d) {
         if (!d.r1.data || d.r1.data != d.x.data || d.r1.coff != d.x.coff || d.r1_cn != 0) return false;
         if (d.cout != C::CT || d.slope != 1.f || d.y2.data || d.m.data || d.shuffle != 1) return false;
         const float inv = 1.f / d.s1;
-        return (float)(__bf16)inv == inv;
+        if constexpr (C::H) return (float)(_Float16)inv == inv;
+        else return (float)(__bf16)inv == inv;
     }
 }
 
@@ -210,13 +213,13 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
                         load16_hx<HX>(d.m, d.n, view_at(d.m, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8));
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
-                        if (!((float)mq[k] > 0.f)) v[k] *= d.mslope;
+                        if (!(elt<C::H>(mq, k) > 0.f)) v[k] *= d.mslope;
                 }
                 if (!(yy < d.h && x0 + xc < d.w)) {
 #pragma unroll
                     for (int k = 0; k < 8; ++k) v[k] = 0.f;
                 }
-                store8_bf16_hx<HX>(d.y, d.n, view_at(d.y, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8), v);
+                store8_bf16_hx<HX, C::H>(d.y, d.n, view_at(d.y, img, 2 * yy + si, 2 * x0 + xo, ct * (CT / 4) + cg * 8), v);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
@@ -283,20 +286,20 @@ __device__ __forceinline__ void epilogue(const Desc& d, f32x16 (&acc)[C::R][C::N
                 for (int e = 0; e < 8; ++e) {
                     u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
                     if constexpr (MODE & 32) u[e] = u[e] * d.s1;
-                    if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (use_r1 ? (float)q1[cb][blk][e] : 0.f);
+                    if constexpr (MODE & 1) u[e] = u[e] * d.s1 + (use_r1 ? elt<C::H>(q1[cb][blk], e) : 0.f);
                     if constexpr (MODE & 2) {
-                        u[e] = u[e] * d.s2 + (float)q2[cb][blk][e];
+                        u[e] = u[e] * d.s2 + elt<C::H>(q2[cb][blk], e);
                     } else {
                         if (scale2) u[e] *= d.s2;
                     }
                     if constexpr (MODE & 16) {
-                        if (use_m && !((float)qm[cb][blk][e] > 0.f)) u[e] *= d.mslope;
+                        if (use_m && !(elt<C::H>(qm[cb][blk], e) > 0.f)) u[e] *= d.mslope;
                     }
                     if (!valid) u[e] = 0.f;
                 }
                 const int co = cf + 16 * blk + 8 * hh;
-                store8_bf16_hx<HX>(d.y, d.n, view_at(d.y, img, yy, xx, co), u);
-                if constexpr (MODE & 4) store8_bf16_hx<HX>(d.y2, d.n, view_at(d.y2, img, yy, xx, co), u);
+                store8_bf16_hx<HX, C::H>(d.y, d.n, view_at(d.y, img, yy, xx, co), u);
+                if constexpr (MODE & 4) store8_bf16_hx<HX, C::H>(d.y2, d.n, view_at(d.y2, img, yy, xx, co), u);
             }
         }
     }
@@ -342,7 +345,7 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
     // (A = (1/s1) I, exact in bf16) and the epilogue computes acc * s1 — no r1 re-read.  The
     // same MFMA order as trunk.hip's kernel, so every path stays bit-identical.
     const bool fold = fold_ok<C, XS2>(d);
-    const uint32_t fidv = C::FOLD ? fold_idv(d.s1) : 0u;
+    const uint32_t fidv = C::FOLD ? fold_idv<C::H>(d.s1) : 0u;
     conv_stamp(0, srow);
 
     // ---- per-lane glds source offsets (chunk-invariant) -------------------
@@ -583,7 +586,7 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
                             if (r >= 0 && r < R) {
     #pragma unroll
                                 for (int f = 0; f < NF; ++f) {
-                                    acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
+                                    acc[r][f] = mfma32t<C::H>(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
                                     if (st + 1 < NS)
                                         for (int k = m * NRD / NM; k < (m + 1) * NRD / NM; ++k) read_one(st + 1, k, cur ^ 1);
                                     __builtin_amdgcn_sched_barrier(0);  // pin the (MFMA, reads) order
@@ -597,7 +600,7 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
                             // (0..3) is a compile-time constant here, so the target accumulator is too
                             if (st == 1 && ia >= 1 && ia <= R) {
                                 const bf16x8 a = fold_a(fidv, FC & 1);
-                                acc[ia - 1][FC >> 1] = mfma32(a, fa[cur][ia], acc[ia - 1][FC >> 1]);
+                                acc[ia - 1][FC >> 1] = mfma32t<C::H>(a, fa[cur][ia], acc[ia - 1][FC >> 1]);
                                 __builtin_amdgcn_sched_barrier(0);
                             }
                         }
@@ -623,7 +626,7 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
                                 if constexpr (C::ABL & 1) {
                                     asm volatile("" ::"v"(fa[cur][ia]), "v"(fb[cur][dyi][f]));
                                 } else {
-                                    acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
+                                    acc[r][f] = mfma32t<C::H>(fb[cur][dyi][f], fa[cur][ia], acc[r][f]);
                                 }
                             }
                         }
@@ -747,6 +750,11 @@ using V_W2 = C3<2, 4, 2, 32, 2>; // 8x32, KC32
 using V_W3 = C3<2, 4, 2, 16, 2, 0, 0, 2>; // 8x32 tile, interleaved
 using V_F0 = C3<4, 4, 2, 16, 2, 192, 0, 2>; // RDB final conv 192→64: V_W0 with compile-time cin, PIPE 2
 using V_F0F = C3<4, 4, 2, 16, 2, 192, 0, 2, 4, 0, 0, 0, 1>; // V_F0 with the residual fold (r1 == x)
+// fp16 storage (isr_conv_desc.f16: the inference path) — the same four production tiles
+using V_G0H = C3<4, 4, 1, 16, 2, 0, 0, 2, 4, 0, 0, 0, 0, 1>;
+using V_W0H = C3<4, 4, 2, 16, 2, 0, 0, 2, 4, 0, 0, 0, 0, 1>;
+using V_F0H = C3<4, 4, 2, 16, 2, 192, 0, 2, 4, 0, 0, 0, 0, 1>;
+using V_F0FH = C3<4, 4, 2, 16, 2, 192, 0, 2, 4, 0, 0, 0, 1, 1>;
 
 // Host mirror of fold_ok: r1 is the conv's own input channels [0, cout), identity activation,
 // 1/s1 exact in bf16 (its low 16 fp32 bits zero).
@@ -757,10 +765,19 @@ static bool fold_host(const isr_conv_desc* d) {
     const float inv = 1.f / d->s1;
     uint32_t bits;
     memcpy(&bits, &inv, 4);
+    if (d->f16) {  // exact in fp16: 10 mantissa bits, a normal fp16 exponent
+        const int ex = (int)((bits >> 23) & 0xff) - 127;
+        return (bits & 0x1fffu) == 0 && ex >= -14 && ex <= 15;
+    }
     return (bits & 0xffffu) == 0;
 }
 
 int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
+    if (d->f16) {  // fp16 storage: the production tiles only (the inference forward)
+        if (variant != 0 || d->x_sub2 || d->taps || d->m.data) return -2;
+        if (d->cout % 64) return launch3x3<V_G0H>(d, s);
+        return d->cin == 192 ? (fold_host(d) ? launch3x3<V_F0FH>(d, s) : launch3x3<V_F0H>(d, s)) : launch3x3<V_W0H>(d, s);
+    }
     if (d->cout % 64) {  // 32-cout tiles: growth convs (cout 32) and dgrad of them (96, 160)
         switch (variant) {
             case 0: return launch3x3<V_G0, true>(d, s);
@@ -1066,6 +1083,7 @@ int chain_knobs_set(const int*) { return -2; }
 #endif
 
 int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) {
+    if (d->f16) return conv3x3_fwd_variant(d, 0, s);
     if (d->taps == 1) return d->cout % 64 ? -2 : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 1, 1>, true>(d, s);
     if (d->taps == 2) return d->cout % 64 ? -2 : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 0, 4, 1, 2>, true>(d, s);
     return conv3x3_fwd_variant(d, 0, s);
@@ -1078,7 +1096,8 @@ int conv3x3_fwd_dispatch(const isr_conv_desc* d, hipStream_t s) {
 // scale * W[co(ci')][n][8 - tap] (180° rotation), where with sub2 the input
 // channel ci' = s*(layer cout/4) + c stands for layer channel co = 4c + s
 // (PixelShuffle order, see isr_conv_desc.x_sub2).
-__device__ __forceinline__ void pack3x3_range(const float* __restrict__ w, __bf16* __restrict__ out, int pcout,
+template <class OT = __bf16>
+__device__ __forceinline__ void pack3x3_range(const float* __restrict__ w, OT* __restrict__ out, int pcout,
                                               int pcin, int transposed, int sub2, float scale, size_t first,
                                               size_t stride, int src_n0 = 0, int src_cin = 0) {
     // dgrad window: packed output channel n = layer input channel src_n0 + n of a layer with
@@ -1102,14 +1121,15 @@ __device__ __forceinline__ void pack3x3_range(const float* __restrict__ w, __bf1
             const int co = sub2 ? (ci % cs4) * 4 + ci / cs4 : ci;  // layer output channel
             v = w[((size_t)co * wrow + src_n0 + n) * 9 + (8 - tap)];  // layer W[co][n0 + n][8 - tap]
         }
-        out[idx] = (__bf16)(v * scale);
+        out[idx] = (OT)(v * scale);
     }
 }
 
-__global__ void pack3x3_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int pcout, int pcin,
+template <class OT>
+__global__ void pack3x3_kernel(const float* __restrict__ w, OT* __restrict__ out, int pcout, int pcin,
                                int transposed, int sub2, float scale) {
-    pack3x3_range(w, out, pcout, pcin, transposed, sub2, scale, blockIdx.x * (size_t)blockDim.x + threadIdx.x,
-                  (size_t)gridDim.x * blockDim.x);
+    pack3x3_range<OT>(w, out, pcout, pcin, transposed, sub2, scale, blockIdx.x * (size_t)blockDim.x + threadIdx.x,
+                      (size_t)gridDim.x * blockDim.x);
 }
 
 // Many packs in one launch (the training plan repacks every conv each step):
@@ -1133,13 +1153,22 @@ static int pack_launch(const float* w, void* out, int pcout, int pcin, int trans
                        hipStream_t s) {
     const size_t total = conv3x3_packed_bytes(pcout, pcin) / 2;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    hipLaunchKernelGGL(pack3x3_kernel, dim3(blocks), dim3(256), 0, s, w, (__bf16*)out, pcout, pcin, transposed, sub2,
-                       scale);
+    hipLaunchKernelGGL(pack3x3_kernel<__bf16>, dim3(blocks), dim3(256), 0, s, w, (__bf16*)out, pcout, pcin, transposed,
+                       sub2, scale);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s) {
     return pack_launch(w, out, cout, cin, 0, 0, 1.f, s);
+}
+
+// the forward pack in fp16 (isr_conv_desc.f16): same layout and size
+int conv3x3_pack_f16(const float* w, void* out, int cout, int cin, hipStream_t s) {
+    const size_t total = conv3x3_packed_bytes(cout, cin) / 2;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(pack3x3_kernel<_Float16>, dim3(blocks), dim3(256), 0, s, w, (_Float16*)out, cout, cin, 0, 0,
+                       1.f);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // layer weights [cout][cin][3][3] → packed dgrad conv (cout' = cin, cin' = cout)

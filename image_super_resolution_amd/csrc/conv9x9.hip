@@ -29,6 +29,7 @@ constexpr int LDS = EP_BYTES > HALO_BYTES ? EP_BYTES : HALO_BYTES;
 
 // packed head weights: [ky 9][ks 3][n 64][k 16] bf16,
 // k = 8h + e → column tap t = 4ks + 2h + (e>>2), channel c = e & 3 (zero if t>=9 or c>=3).
+template <bool H>
 __global__ __launch_bounds__(256) void head9x9_kernel(isr_head_desc d) {
     using namespace head;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -55,10 +56,17 @@ __global__ __launch_bounds__(256) void head9x9_kernel(isr_head_desc d) {
                 for (int c = 0; c < 3; ++c) v[c] = xp[o + c * plane];
             }
         }
-        bf16x4 t;
+        if constexpr (H) {
+            f16x4 t;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] = (__bf16)v[c];
-        *reinterpret_cast<bf16x4*>(smem + p * 8) = t;
+            for (int c = 0; c < 4; ++c) t[c] = (_Float16)v[c];
+            *reinterpret_cast<f16x4*>(smem + p * 8) = t;
+        } else {
+            bf16x4 t;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) t[c] = (__bf16)v[c];
+            *reinterpret_cast<bf16x4*>(smem + p * 8) = t;
+        }
     }
     __syncthreads();
 
@@ -92,7 +100,7 @@ __global__ __launch_bounds__(256) void head9x9_kernel(isr_head_desc d) {
                 const int r = i - ky;
                 if (r >= 0 && r < R) {
 #pragma unroll
-                    for (int f = 0; f < NF; ++f) acc[r][f] = mfma32(a, b[ky][f], acc[r][f]);
+                    for (int f = 0; f < NF; ++f) acc[r][f] = mfma32t<H>(a, b[ky][f], acc[r][f]);
                 }
             }
         }
@@ -128,12 +136,13 @@ __global__ __launch_bounds__(256) void head9x9_kernel(isr_head_desc d) {
             const float* src = ep + px * EPS + cg * 8;
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = src[k];
-            epi_plain8(e, v, img, y0 + wave * R + r, x0 + px, cg * 8);
+            epi_plain8<H>(e, v, img, y0 + wave * R + r, x0 + px, cg * 8);
         }
     }
 }
 
-__global__ void pack_head_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
+template <class OT>
+__global__ void pack_head_kernel(const float* __restrict__ w, OT* __restrict__ out, int cout, int cin) {
     const int total = 9 * 3 * cout * 16;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
         int rem = idx;
@@ -145,7 +154,7 @@ __global__ void pack_head_kernel(const float* __restrict__ w, __bf16* __restrict
         const int t = 4 * ks + 2 * hh + (e >> 2), c = e & 3;
         float v = 0.f;
         if (t < 9 && c < cin) v = w[(((size_t)n * cin + c) * 9 + ky) * 9 + t];
-        out[idx] = (__bf16)v;
+        out[idx] = (OT)v;
     }
 }
 
@@ -297,6 +306,7 @@ static_assert(TR * HC % 32 == 0, "");
 static_assert(2 * LDS <= 163840, "two blocks per CU");
 }  // namespace tail8
 
+template <bool H = false>
 __global__ __launch_bounds__(256, 2) void tail9x9_k8_kernel(isr_tail_desc d) {
     using namespace tail8;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -346,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void tail9x9_k8_kernel(isr_tail_desc d) {
 #pragma unroll
                 for (int t = 0; t < RT; ++t) {
                     const int q = (wave * RT + t) * HC + kx + l31;
-                    acc[t] = mfma32(lds_read16(hp + halo_unit2(q, hh) * 16), b, acc[t]);
+                    acc[t] = mfma32t<H>(lds_read16(hp + halo_unit2(q, hh) * 16), b, acc[t]);
                 }
             }
         }
@@ -909,7 +919,7 @@ constexpr int ST = 2;
 static_assert(LDS <= 163840, "LDS");
 }  // namespace tail8w
 
-template <int ABL, int PD = tail8w::PD>
+template <int ABL, int PD = tail8w::PD, bool H = false>
 __global__ __launch_bounds__(512, 1) void tail9x9_stream8_kernel(isr_tail_desc d, int sh) {
     using namespace tail8w;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1030,7 +1040,7 @@ __global__ __launch_bounds__(512, 1) void tail9x9_stream8_kernel(isr_tail_desc d
                 if constexpr (ABL & 1) {
                     asm volatile("" ::"v"(fa[s2 % PD]), "v"(wr[s2]));
                 } else {
-                    acc = mfma32(fa[s2 % PD], wr[s2], acc);
+                    acc = mfma32t<H>(fa[s2 % PD], wr[s2], acc);
                 }
                 if (s2 + PD < 36) rd(s2 + PD, s2 % PD);
                 if (s2 >= 1 && s2 <= ROW_INSTR && dma_on) dma(i + 1, s2 - 1);
@@ -1242,7 +1252,8 @@ __global__ __launch_bounds__(256, MINB) void tail9x9_lane_kernel(isr_tail_desc d
     }
 }
 
-__global__ void pack_tail_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int cout, int cin) {
+template <class OT>
+__global__ void pack_tail_kernel(const float* __restrict__ w, OT* __restrict__ out, int cout, int cin) {
     const int total = tail::W_BYTES / 2;
     for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
         int rem = idx;
@@ -1257,16 +1268,19 @@ __global__ void pack_tail_kernel(const float* __restrict__ w, __bf16* __restrict
         const int ci = chunk * 32 + ks * 16 + hh * 8 + e;
         float v = 0.f;
         if (n < 27 && co < cout) v = w[(((size_t)co * cin + ci) * 9 + ky) * 9 + kx];
-        out[idx] = (__bf16)v;
+        out[idx] = (OT)v;
     }
 }
 
 // ============================== launchers ================================
 int head9x9_fwd_dispatch(const isr_head_desc* d, hipStream_t s) {
-    lds_limit((const void*)head9x9_kernel, head::LDS);
     dim3 grid(d->wa / head::TW, d->ha / head::TH, d->n);
-    hipLaunchKernelGGL(head9x9_kernel, grid, dim3(256), head::LDS, s, *d);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    auto go = [&](auto kern) {
+        lds_limit((const void*)kern, head::LDS);
+        hipLaunchKernelGGL(kern, grid, dim3(256), head::LDS, s, *d);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    };
+    return d->f16 ? go(head9x9_kernel<true>) : go(head9x9_kernel<false>);
 }
 
 int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
@@ -1275,6 +1289,16 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
     // walk (4) and 236-280 us for the lane-streaming walk (6), all bit-identical
     // (tools/tune_tail.py, tests/test_gpu_kernels.py); the persistent variant 2 measures 515 us
     if (variant == 0) variant = 5;
+    if (d->f16) {  // fp16 activations (the inference path): the production walk and its fallback only
+        if (variant != 5 && variant != 3) return -2;
+        if (variant == 5 && (size_t)3 * d->h * d->w * (d->y_u8 ? 1 : 4) >= ((size_t)1 << 31)) variant = 3;
+        if (variant == 3) {
+            lds_limit((const void*)tail9x9_k8_kernel<true>, tail8::LDS);
+            dim3 grid8(d->wa / tail8::TW, d->ha / tail8::TH, d->n);
+            hipLaunchKernelGGL(tail9x9_k8_kernel<true>, grid8, dim3(256), tail8::LDS, s, *d);
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+        }
+    }
 #ifndef ISR_TUNING
     // production: the row-streaming walk (5) and the 8-row per-tile kernel (3, the fallback of
     // images whose fp32 output passes 2 GiB); the other forms are in the tuning library only
@@ -1380,7 +1404,7 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
             case 5: return go(tail9x9_stream8_kernel<0, 5>);
             case 6: return go(tail9x9_stream8_kernel<0, 6>);
 #endif
-            default: return go(tail9x9_stream8_kernel<0>);
+            default: return d->f16 ? go(tail9x9_stream8_kernel<0, tail8w::PD, true>) : go(tail9x9_stream8_kernel<0>);
         }
     }
 #ifdef ISR_TUNING
@@ -1416,9 +1440,9 @@ int tail9x9_fwd_variant(const isr_tail_desc* d, int variant, hipStream_t s) {
     }
 #endif
     if (variant == 3) {
-        lds_limit((const void*)tail9x9_k8_kernel, tail8::LDS);
+        lds_limit((const void*)tail9x9_k8_kernel<false>, tail8::LDS);
         dim3 grid8(d->wa / tail8::TW, d->ha / tail8::TH, d->n);
-        hipLaunchKernelGGL(tail9x9_k8_kernel, grid8, dim3(256), tail8::LDS, s, *d);
+        hipLaunchKernelGGL(tail9x9_k8_kernel<false>, grid8, dim3(256), tail8::LDS, s, *d);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
 #ifdef ISR_TUNING
@@ -1445,13 +1469,16 @@ int tail9x9_fwd_dispatch(const isr_tail_desc* d, hipStream_t s) { return tail9x9
 size_t head9x9_packed_bytes(int cout) { return (size_t)9 * 3 * cout * 16 * 2; }
 size_t tail9x9_packed_bytes() { return tail::W_BYTES; }
 
-int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s) {
-    hipLaunchKernelGGL(pack_head_kernel, dim3(64), dim3(256), 0, s, w, (__bf16*)out, cout, cin);
+// h: fp16 weights (the isr_*_desc.f16 forms), else bf16; same layout and size
+int head9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s, bool h) {
+    if (h) hipLaunchKernelGGL(pack_head_kernel<_Float16>, dim3(64), dim3(256), 0, s, w, (_Float16*)out, cout, cin);
+    else hipLaunchKernelGGL(pack_head_kernel<__bf16>, dim3(64), dim3(256), 0, s, w, (__bf16*)out, cout, cin);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s) {
-    hipLaunchKernelGGL(pack_tail_kernel, dim3(64), dim3(256), 0, s, w, (__bf16*)out, cout, cin);
+int tail9x9_pack(const float* w, void* out, int cout, int cin, hipStream_t s, bool h) {
+    if (h) hipLaunchKernelGGL(pack_tail_kernel<_Float16>, dim3(64), dim3(256), 0, s, w, (_Float16*)out, cout, cin);
+    else hipLaunchKernelGGL(pack_tail_kernel<__bf16>, dim3(64), dim3(256), 0, s, w, (__bf16*)out, cout, cin);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -19,11 +19,59 @@ typedef __attribute__((ext_vector_type(8))) float f32x8;
 
 #define ISR_LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+
 // One 32x32x16 bf16 MFMA: acc += A(32x16) * B(16x32).
 // Lane l (r = l & 31, h = l >> 5) supplies A[r][8h..8h+7] and B[8h..8h+7][r];
 // accumulator register g of lane l holds D[(g&3) + 8*(g>>2) + 4*h][r].
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 acc) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+}
+
+// Storage type of activations and packed weights, a compile-time choice per kernel: H = false →
+// bf16 (training, the per-conv backward), H = true → fp16 (the inference path, isr_conv_desc.f16:
+// 10 mantissa bits instead of 7 at the same MFMA rate, v_mfma_f32_32x32x16_f16 with the same
+// fragment layout).  Fragments travel as 16-byte bf16x8 containers; only the MFMA and the
+// float conversions at the epilogue / loads look at the type.
+template <bool H>
+__device__ __forceinline__ f32x16 mfma32t(bf16x8 a, bf16x8 b, f32x16 acc) {
+    if constexpr (H) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc,
+                                                      0, 0, 0);
+    } else {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    }
+}
+
+// element e of an 8-element storage vector as float
+template <bool H>
+__device__ __forceinline__ float elt(bf16x8 v, int e) {
+    if constexpr (H) return (float)__builtin_bit_cast(f16x8, v)[e];
+    else return (float)v[e];
+}
+
+// 8 floats → one 16-byte storage vector (round to nearest even)
+template <bool H>
+__device__ __forceinline__ bf16x8 pack8(const float* x) {
+    if constexpr (H) {
+        f16x8 t;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = (_Float16)x[e];
+        return __builtin_bit_cast(bf16x8, t);
+    } else {
+        bf16x8 t;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = (__bf16)x[e];
+        return t;
+    }
+}
+
+// the storage bits of one float (16 bits, in the low half)
+template <bool H>
+__device__ __forceinline__ uint16_t bits16(float x) {
+    if constexpr (H) return __builtin_bit_cast(uint16_t, (_Float16)x);
+    else return __builtin_bit_cast(uint16_t, (__bf16)x);
 }
 
 __device__ __forceinline__ void swap_halves(float& lo, float& hi) {
@@ -113,6 +161,18 @@ __device__ __forceinline__ void store8_bf16(char* p, const float* v) {
     *reinterpret_cast<bf16x8*>(p) = t;
 }
 
+template <bool H>
+__device__ __forceinline__ void load8_t(const char* p, float* v) {
+    const bf16x8 t = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = elt<H>(t, e);
+}
+
+template <bool H>
+__device__ __forceinline__ void store8_t(char* p, const float* v) {
+    *reinterpret_cast<bf16x8*>(p) = pack8<H>(v);
+}
+
 // 16-byte load / 8-channel bf16 store at `p` inside view `v`: plain (HX = 0), or the hand-off
 // form (HX = 1: sc1 load that bypasses L1; write-through sc1 store, Guideline 16 R1) through a
 // buffer descriptor built from the view's base (wave-uniform: no waterfall) with the byte
@@ -138,11 +198,9 @@ __device__ __forceinline__ bf16x8 load16_hx(const V& v, int n, const char* p) {
     }
 }
 
-template <int HX, class V>
+template <int HX, bool H = false, class V>
 __device__ __forceinline__ void store8_bf16_hx(const V& v, int n, char* p, const float* x) {
-    bf16x8 t;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) t[e] = (__bf16)x[e];
+    const bf16x8 t = pack8<H>(x);
     if constexpr (HX) {
         typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
         const int off = (int)(p - (const char*)v.data);
@@ -163,6 +221,7 @@ struct Epi {
     int h, w;
 };
 
+template <bool H = false>
 __device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int yy, int xx, int co) {
     if (e.bias) {
         f32x4 b0 = *reinterpret_cast<const f32x4*>(e.bias + co);
@@ -175,19 +234,19 @@ __device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int 
     const bool valid = (yy < e.h) && (xx < e.w);
     if (e.r1.data) {
         float r[8];
-        load8_bf16(view_at(e.r1, img, yy, xx, co), r);
+        load8_t<H>(view_at(e.r1, img, yy, xx, co), r);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = v[k] * e.s1 + r[k];
     }
     if (e.r2.data) {
         float r[8];
-        load8_bf16(view_at(e.r2, img, yy, xx, co), r);
+        load8_t<H>(view_at(e.r2, img, yy, xx, co), r);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = v[k] * e.s2 + r[k];
     }
     if (e.m.data) {
         float m[8];
-        load8_bf16(view_at(e.m, img, yy, xx, co), m);
+        load8_t<H>(view_at(e.m, img, yy, xx, co), m);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = m[k] > 0.f ? v[k] : v[k] * e.mslope;
     }
@@ -195,8 +254,8 @@ __device__ __forceinline__ void epi_plain8(const Epi& e, float* v, int img, int 
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = 0.f;
     }
-    store8_bf16(view_at(e.y, img, yy, xx, co), v);
-    if (e.y2.data) store8_bf16(view_at(e.y2, img, yy, xx, co), v);
+    store8_t<H>(view_at(e.y, img, yy, xx, co), v);
+    if (e.y2.data) store8_t<H>(view_at(e.y2, img, yy, xx, co), v);
 }
 
 // Raise `kern`'s dynamic-LDS limit to `bytes` once per (kernel, device, host thread).  The

@@ -39,7 +39,8 @@ size_t trunk_state_words(int n, int ha, int wa) {
 // 32 residual form, 64 a 16-channel plane of 2 GiB or more (one buffer resource spans one plane),
 // 128 too many layers.
 __global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* layers, const int32_t* kinds, int nl,
-                                                          int n, int ha, int wa, unsigned* state, int th) {
+                                                          int n, int ha, int wa, unsigned* state, int th,
+                                                          int h16) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     unsigned* err = reinterpret_cast<unsigned*>(smem);
     const int L = threadIdx.x;
@@ -64,17 +65,26 @@ __global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* l
         if (!same_geo(d.x) || !same_geo(d.y) || (d.r2.data && !same_geo(d.r2)) || (masked && !same_geo(d.m))) e |= 2;
         if (kind == 0 || kind == 2 ? d.cout != 32 : (kind == 1 ? d.cout != 64 : true)) e |= 4;
         if (d.cin % 16 || d.cin < 64 || d.cin / 16 > 120 || !d.bias || ((uintptr_t)d.bias & 15)) e |= 8;
-        if (d.shuffle != 1 || d.x_sub2 || d.taps || d.y2.data || (d.m.data != nullptr) != masked ||
+        if (d.f16 != h16 || d.shuffle != 1 || d.x_sub2 || d.taps || d.y2.data || (d.m.data != nullptr) != masked ||
             (masked && (d.m_c0 != 0 || d.slope != 1.f || d.r1.data || d.r2.data || d.s1 != 1.f || d.s2 != 1.f)))
             e |= 16;
         int fold = 0;
         uint16_t idv = 0;
         if (d.r1.data) {
+            // A = (1/s1) I must be exact in the storage type (the chain's f16 flag)
             const float inv = 1.f / d.s1;
-            const __bf16 bi = (__bf16)inv;
-            idv = __builtin_bit_cast(uint16_t, bi);
+            float back;
+            if (h16) {
+                const _Float16 hi = (_Float16)inv;
+                idv = __builtin_bit_cast(uint16_t, hi);
+                back = (float)hi;
+            } else {
+                const __bf16 bi = (__bf16)inv;
+                idv = __builtin_bit_cast(uint16_t, bi);
+                back = (float)bi;
+            }
             const bool alias = d.r1.data == d.x.data && d.r1.coff == d.x.coff && d.r1_cn == 0;
-            if (!alias || kind != 1 || d.slope != 1.f || (float)bi != inv) e |= 32;
+            if (!alias || kind != 1 || d.slope != 1.f || back != inv) e |= 32;
             fold = 1;
         } else if (d.r2.data) {
             e |= 32;
@@ -128,7 +138,7 @@ __global__ __launch_bounds__(1024) void trunk_prep_kernel(const isr_conv_desc* l
 
 int trunk_prep_launch(const isr_chain_desc* cd, int th, hipStream_t s) {
     hipLaunchKernelGGL(trunk_prep_kernel, dim3(1), dim3(1024), 16, s, cd->layers, cd->kinds, cd->nl, cd->n, cd->ha,
-                       cd->wa, cd->state, th);
+                       cd->wa, cd->state, th, cd->f16 ? 1 : 0);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -524,7 +534,7 @@ __device__ __forceinline__ void force_publish(const TrunkCtx<K>& c, Stream<K>& s
     st.pend_t = -1;
 }
 
-template <class K, int NF, bool MASKED = false>
+template <class K, int NF, bool MASKED = false, bool H = false>
 __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, const_rec& rec, int L, int t,
                                          const Next& nx) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -745,13 +755,13 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                         } else
 #endif
     #pragma unroll
-                        for (int f = 0; f < NF; ++f) acc[r][f] = mfma32(fb[cur][dyi][f], fa[cur][r + dyi], acc[r][f]);
+                        for (int f = 0; f < NF; ++f) acc[r][f] = mfma32t<H>(fb[cur][dyi][f], fa[cur][r + dyi], acc[r][f]);
                         if constexpr (NF == 2 && FC >= 0) {
                             // residual fold: + x/s1 on the centre pixels of row r (dx = 1, dy = 1),
                             // between the row's dy = 1 and dy = 2 contributions (chunk FC, compile-time)
                             if (dyi == 1 && stp == 1) {
                                 const bf16x8 a = fold_a_bits<K::NSET == 1>(idv, FC & 1);
-                                acc[r][FC >> 1] = mfma32(a, fa[cur][r + 1], acc[r][FC >> 1]);
+                                acc[r][FC >> 1] = mfma32t<H>(a, fa[cur][r + 1], acc[r][FC >> 1]);
                             }
                         }
                         // input row ia = r + dyi is last used here when dyi == min(2, ia)
@@ -851,12 +861,12 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         if (masked)
-                            u[e] = (float)q2[r][f][blk][e] > 0.f ? u[e] : u[e] * slope;
+                            u[e] = elt<H>(q2[r][f][blk], e) > 0.f ? u[e] : u[e] * slope;
                         else
                             u[e] = u[e] >= 0.f ? u[e] : u[e] * slope;
                         if (fold) u[e] = u[e] * s1;
                         if (has_r2) {
-                            u[e] = u[e] * s2 + (float)q2[r][f][blk][e];
+                            u[e] = u[e] * s2 + elt<H>(q2[r][f][blk], e);
                         } else {
                             if (scale2) u[e] *= s2;
                         }
@@ -864,9 +874,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
                     }
                     const auto yr = rsrc_n(ybase + (size_t)(2 * f + blk) * c.pstride, c.pstride);
                     const uint32_t off = pix * 32 + 16 * hh;
-                    bf16x8 tq;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) tq[e] = (__bf16)u[e];
+                    const bf16x8 tq = pack8<H>(u);
                     if (!(c.abl & 4)) {
                         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tq), yr, off, 0, K::STORE_AUX);
                         ++st.issued;
@@ -882,7 +890,7 @@ __device__ __forceinline__ void run_tile(const TrunkCtx<K>& c, Stream<K>& st, co
     ++st.tseq;
 }
 
-template <class K>
+template <class K, bool H = false>
 __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
     TrunkCtx<K> c;
     c.state = a.state;
@@ -957,9 +965,9 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
                     nx.self_dep = im == im2 && abs(bx - bx2) <= 1 && abs(by - by2) <= 1;
                 }
                 const int kind = rec_kind(rec);
-                if (kind == 0) run_tile<K, 1>(c, st, rec, L, t, nx);
-                else if (kind == 2) run_tile<K, 1, true>(c, st, rec, L, t, nx);  // the backward chain's gathers
-                else run_tile<K, 2>(c, st, rec, L, t, nx);
+                if (kind == 0) run_tile<K, 1, false, H>(c, st, rec, L, t, nx);
+                else if (kind == 2) run_tile<K, 1, true, H>(c, st, rec, L, t, nx);  // the backward chain's gathers
+                else run_tile<K, 2, false, H>(c, st, rec, L, t, nx);
             }
         }
     }
@@ -972,7 +980,7 @@ __global__ __launch_bounds__(K::NT, K::WPS) void trunk_kernel(TrunkArgs a) {
 // Grid: every workgroup must be resident at once (tiles wait on other workgroups' tiles), so
 // the grid is min(tiles, resident workgroups) with residency from the occupancy API (capped at
 // what the build is made for); ISR_ERR when that is below one workgroup per CU.
-template <class K>
+template <class K, bool H = false>
 static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
     if (cd->ha % K::TH || cd->wa % tk::TW || cd->nl < 1 || cd->nl > 1024) return -2;
     const int nbx = cd->wa / tk::TW, nby = cd->ha / K::TH;
@@ -981,7 +989,7 @@ static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
     static thread_local int cached_dev = -1, cached_per_cu = 0, cached_cus = 0;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
-    const void* kern = (const void*)trunk_kernel<K>;
+    const void* kern = (const void*)trunk_kernel<K, H>;
     if (dev != cached_dev) {
         (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
         int per_cu = 0;
@@ -1006,7 +1014,7 @@ static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
     a.rec_off = rec_off;
     a.nl = cd->nl;
     a.acquire = cd->acquire;
-    hipLaunchKernelGGL(trunk_kernel<K>, dim3(grid), dim3(K::NT), K::LDS, s, a);
+    hipLaunchKernelGGL((trunk_kernel<K, H>), dim3(grid), dim3(K::NT), K::LDS, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1040,6 +1048,7 @@ int trunk_lc_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_lc.hip (
 #endif
 
 int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
+    if (cd->f16) return form == 0 ? trunk_launch_k<TK_PAIR, true>(cd, s) : -3;  // fp16 storage: production form only
     if (form == 0) return trunk_launch_k<TK_PAIR>(cd, s);
 #ifdef ISR_TUNING
     if (form == 8) return trunk_lc_launch(cd, s);

@@ -47,7 +47,11 @@ def _require_gpu(t: torch.Tensor, what: str) -> None:
 
 @dataclass
 class ActBuffer:
-    """Channel-blocked bf16 activation buffer [n][c/16][ha+2p][wa+2p][16], zero border p.
+    """Channel-blocked activation buffer [n][c/16][ha+2p][wa+2p][16], zero border p.
+
+    Storage is bf16 (training: the per-conv forward and backward) or fp16 (the inference
+    forward, isr_conv_desc.f16 — 3 more mantissa bits at the same MFMA rate and footprint;
+    the generator's activations stay far inside fp16 range).
 
     Each 16-channel block is a contiguous plane, so a conv K-chunk reads whole
     cache lines.  (h, w) is the valid image size, (ha, wa) the tile-aligned
@@ -64,20 +68,28 @@ class ActBuffer:
 
     @staticmethod
     def alloc(n: int, h: int, w: int, c: int, pad: int, device, ha: int | None = None,
-              wa: int | None = None, min_hp: int = 0, min_wp: int = 0) -> "ActBuffer":
+              wa: int | None = None, min_hp: int = 0, min_wp: int = 0,
+              dtype: torch.dtype = torch.bfloat16) -> "ActBuffer":
         """min_hp / min_wp: extra zero rows / columns below / right of the computed
         region (a stride-2 consumer reads 2*ha_out + 2*pad rows of its input)."""
+        if dtype not in (torch.bfloat16, torch.float16):
+            raise TypeError(f"ActBuffer storage must be bfloat16 or float16, got {dtype}")
         if c % 16:
             raise ValueError(f"ActBuffer channels must be a multiple of 16, got {c}")
         ha = round_up(h, TILE_H) if ha is None else ha
         wa = round_up(w, TILE_W) if wa is None else wa
         hp, wp = max(ha + 2 * pad, min_hp), max(wa + 2 * pad, min_wp)
-        t = torch.zeros((n, c // 16, hp, wp, 16), dtype=torch.bfloat16, device=device)
+        t = torch.zeros((n, c // 16, hp, wp, 16), dtype=dtype, device=device)
         return ActBuffer(t, n, h, w, ha, wa, pad)
 
     @property
     def c(self) -> int:
         return self.t.shape[1] * 16
+
+    @property
+    def f16(self) -> int:
+        """1 for fp16 storage (the descriptors' f16 field), 0 for bf16."""
+        return int(self.t.dtype == torch.float16)
 
     def view(self, coff: int = 0) -> IsrView:
         return IsrView(self.t.data_ptr(), self.t.shape[2], self.t.shape[3], self.c, self.pad, coff)
@@ -96,7 +108,7 @@ class ActBuffer:
             raise ValueError("set_nchw: channel block / shape mismatch")
         p = self.pad
         self.t[:, c0 // 16:(c0 + c) // 16, p:p + h, p:p + w, :] = (
-            x.reshape(n, c // 16, 16, h, w).permute(0, 1, 3, 4, 2).to(torch.bfloat16))
+            x.reshape(n, c // 16, 16, h, w).permute(0, 1, 3, 4, 2).to(self.t.dtype))
 
     def outside_valid(self) -> torch.Tensor:
         """Every element outside the valid h x w region (border + alignment slack)."""
@@ -106,9 +118,10 @@ class ActBuffer:
         return self.t[mask]
 
     @staticmethod
-    def from_nchw(x: torch.Tensor, pad: int = 1, c_alloc: int | None = None) -> "ActBuffer":
+    def from_nchw(x: torch.Tensor, pad: int = 1, c_alloc: int | None = None,
+                  dtype: torch.dtype = torch.bfloat16) -> "ActBuffer":
         n, c, h, w = x.shape
-        buf = ActBuffer.alloc(n, h, w, c_alloc or c, pad, x.device)
+        buf = ActBuffer.alloc(n, h, w, c_alloc or c, pad, x.device, dtype=dtype)
         buf.set_nchw(x, 0)
         return buf
 
@@ -120,18 +133,25 @@ _NULL_VIEW = IsrView(None, 0, 0, 0, 0, 0)
 
 
 # ---------------------------------------------------------------- packing
-def pack_conv3x3(w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """fp32 OIHW [cout, cin, 3, 3] device weights → packed bf16 kernel layout."""
+def _wdtype(f16: bool) -> torch.dtype:
+    return torch.float16 if f16 else torch.bfloat16
+
+
+def pack_conv3x3(w: torch.Tensor, out: torch.Tensor | None = None, f16: bool = False) -> torch.Tensor:
+    """fp32 OIHW [cout, cin, 3, 3] device weights → packed bf16 (fp16 with `f16`: the
+    inference forward, isr_pack_conv3x3_f16) kernel layout."""
     _require_gpu(w, "pack_conv3x3")
     lib = _lib.load()
     cout, cin = w.shape[:2]
     w = w.detach().float().contiguous()
     n = lib.isr_conv3x3_packed_bytes(cout, cin) // 2
+    dt = _wdtype(f16)
     if out is None:
-        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
-    elif out.numel() != n or out.dtype != torch.bfloat16:
+        out = torch.empty(n, dtype=dt, device=w.device)
+    elif out.numel() != n or out.dtype != dt:
         raise ValueError("pack_conv3x3: bad output buffer")
-    check(lib.isr_pack_conv3x3(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_conv3x3")
+    fn = lib.isr_pack_conv3x3_f16 if f16 else lib.isr_pack_conv3x3
+    check(fn(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_conv3x3")
     return out
 
 
@@ -186,31 +206,35 @@ def pack_batch(table: tuple[torch.Tensor, int]) -> None:
     check(_lib.load().isr_pack_conv3x3_batch(t.data_ptr(), n, _stream()), "isr_pack_conv3x3_batch")
 
 
-def pack_head9x9(w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def pack_head9x9(w: torch.Tensor, out: torch.Tensor | None = None, f16: bool = False) -> torch.Tensor:
     _require_gpu(w, "pack_head9x9")
     lib = _lib.load()
     cout, cin = w.shape[:2]
     w = w.detach().float().contiguous()
     n = lib.isr_head9x9_packed_bytes(cout, cin) // 2
+    dt = _wdtype(f16)
     if out is None:
-        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
-    elif out.numel() != n or out.dtype != torch.bfloat16:
+        out = torch.empty(n, dtype=dt, device=w.device)
+    elif out.numel() != n or out.dtype != dt:
         raise ValueError("pack_head9x9: bad output buffer")
-    check(lib.isr_pack_head9x9(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_head9x9")
+    fn = lib.isr_pack_head9x9_f16 if f16 else lib.isr_pack_head9x9
+    check(fn(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_head9x9")
     return out
 
 
-def pack_tail9x9(w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def pack_tail9x9(w: torch.Tensor, out: torch.Tensor | None = None, f16: bool = False) -> torch.Tensor:
     _require_gpu(w, "pack_tail9x9")
     lib = _lib.load()
     cout, cin = w.shape[:2]
     w = w.detach().float().contiguous()
     n = lib.isr_tail9x9_packed_bytes(cout, cin) // 2
+    dt = _wdtype(f16)
     if out is None:
-        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
-    elif out.numel() != n or out.dtype != torch.bfloat16:
+        out = torch.empty(n, dtype=dt, device=w.device)
+    elif out.numel() != n or out.dtype != dt:
         raise ValueError("pack_tail9x9: bad output buffer")
-    check(lib.isr_pack_tail9x9(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_tail9x9")
+    fn = lib.isr_pack_tail9x9_f16 if f16 else lib.isr_pack_tail9x9
+    check(fn(w.data_ptr(), out.data_ptr(), cout, cin, _stream()), "isr_pack_tail9x9")
     return out
 
 
@@ -244,7 +268,17 @@ def conv3x3_desc(x: ActBuffer, cin: int, wpack: torch.Tensor, bias: torch.Tensor
     d.m = m.view(y_coff if m_coff is None else m_coff) if m is not None else _NULL_VIEW
     d.mslope, d.m_c0, d.r1_cn, d.x_sub2 = mslope, m_c0, r1_cn, int(bool(x_sub2))
     d.taps = taps
+    d.f16 = _same_storage("conv3x3", wpack, x, y, y2, r1, r2, m)
     return d
+
+
+def _same_storage(what: str, wpack: torch.Tensor, *bufs) -> int:
+    """The descriptor's f16 flag: every activation buffer and the packed weights of one launch
+    share one storage type (bf16 or fp16)."""
+    dts = {b.t.dtype for b in bufs if b is not None}
+    if len(dts) != 1 or wpack.dtype not in dts:
+        raise TypeError(f"{what}: mixed storage types {sorted(map(str, dts | {wpack.dtype}))}")
+    return int(wpack.dtype == torch.float16)
 
 
 def launch_conv3x3(d: IsrConvDesc) -> None:
@@ -284,6 +318,7 @@ def head9x9_desc(x: torch.Tensor, wpack: torch.Tensor, bias: torch.Tensor | None
     d.slope = slope
     d.m = m.view(0) if m is not None else _NULL_VIEW
     d.mslope = mslope
+    d.f16 = _same_storage("head9x9", wpack, y, y2, m)
     return d
 
 
@@ -310,6 +345,7 @@ def tail9x9_desc(x: ActBuffer, wpack: torch.Tensor, bias: torch.Tensor | None, o
     d.bias = bias.data_ptr() if bias is not None else None
     d.y = out.data_ptr()
     d.y_u8 = 1 if out.dtype == torch.uint8 else 0
+    d.f16 = _same_storage("tail9x9", wpack, x)
     return d
 
 

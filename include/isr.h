@@ -90,6 +90,10 @@ typedef struct isr_conv_desc {
                           A stride-2 3x3 conv (Discriminator, utils/models.py:533-542) is taps=1 over the
                           x_sub2 view with 4*cin phase-expanded weights; its input gradient is taps=2
                           over the output gradient with shuffle == 2 (4*cin phase outputs). */
+    int32_t f16;       /* 0: activations (x, y, y2, r1, r2) and wpack are bf16; 1: fp16 (the inference
+                          path: 10 mantissa bits instead of 7, the storage type of the reference's own
+                          fp16 autocast, train.py:54 / rs.py), wpack from isr_pack_conv3x3_f16.  fp16 is
+                          forward-only: m.data == NULL, x_sub2 == 0, taps == 0. */
 } isr_conv_desc;
 
 /* 9x9 head conv, 3 → cout (=64) channels, input NCHW (fp32 already normalised,
@@ -112,6 +116,7 @@ typedef struct isr_head_desc {
      * LeakyReLU'(m) of slope mslope (the last Scaler's activation). */
     isr_view m;
     float mslope;
+    int32_t f16;           /* 1: y / y2 fp16 and wpack from isr_pack_head9x9_f16 (forward only, m.data == NULL) */
 } isr_head_desc;
 
 /* 9x9 tail conv, cin (=64) → 3 channels, + bias + tanh, NCHW out (fp32, or
@@ -126,6 +131,7 @@ typedef struct isr_tail_desc {
     const float* bias;       /* [3] or NULL */
     void* y;                 /* NCHW [n][3][h][w] */
     int32_t y_u8;            /* 0: fp32 tanh output; 1: uint8 image */
+    int32_t f16;             /* 1: x fp16 and wpack from isr_pack_tail9x9_f16 */
 } isr_tail_desc;
 
 /* Weight / bias gradient of a 3x3 'same' conv (the bwd-weight half of autograd
@@ -344,6 +350,10 @@ size_t isr_head9x9_packed_bytes(int32_t cout, int32_t cin);
 int isr_pack_head9x9(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
 size_t isr_tail9x9_packed_bytes(int32_t cout, int32_t cin);
 int isr_pack_tail9x9(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
+/* The same three packs in fp16 (same layouts and sizes), for descriptors with f16 = 1. */
+int isr_pack_conv3x3_f16(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
+int isr_pack_head9x9_f16(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
+int isr_pack_tail9x9_f16(const float* w_oihw, void* packed, int32_t cout, int32_t cin, isr_stream_t s);
 
 int isr_conv3x3_fwd(const isr_conv_desc* d, isr_stream_t s);
 /* Tuning entry point: same contract as isr_conv3x3_fwd with an explicit kernel
@@ -393,13 +403,14 @@ typedef struct isr_chain_desc {
     int32_t n, ha, wa;
     uint32_t* state;
     int32_t acquire;
+    int32_t f16;    /* every layer's isr_conv_desc.f16 (the table lives in device memory): 1 = fp16 */
 } isr_chain_desc;
 size_t isr_conv_chain_state_words(int32_t n, int32_t ha, int32_t wa);
 int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
 /* The same with the kernel chosen: 0 = production (trunk.hip: one continuous K-chunk stream per
  * workgroup across its (layer, tile) items, waits only before the chunks the previous layer
  * wrote, the RDB residual folded into the MFMAs; needs every view to share (hp, wp, cs, pad),
- * a bias, cin >= 64, r1 (if any) == the layer's own input with slope 1 and 1/s1 exact in bf16 —
+ * a bias, cin >= 64, r1 (if any) == the layer's own input with slope 1 and 1/s1 exact in the storage type (bf16, or fp16 with f16) —
  * a table that breaks this makes the launch give up: state[1] == state[0]); 1 = the round-2
  * kernel (conv3x3.hip: one independent conv tile per (layer, tile)).  Both produce the outputs
  * of the per-layer isr_conv3x3_fwd calls bit for bit.  0 = trunk.hip in its two-workgroups-per-CU

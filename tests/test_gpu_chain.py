@@ -25,10 +25,10 @@ def lib(built_lib):
     return built_lib
 
 
-def _gw(blocks, scale=4, enchant=False, seed=0):
+def _gw(blocks, scale=4, enchant=False, seed=0, f16=True):
     m = (models.EResNet if enchant else models.ResNet)(blocks, 0.2, scaleRate=scale)
     sd = synth_state_dict(m.state_dict(), seed)
-    return engine.pack_generator({k: v.to(DEV) for k, v in sd.items()}, enchant=enchant, device=DEV)
+    return engine.pack_generator({k: v.to(DEV) for k, v in sd.items()}, enchant=enchant, device=DEV, f16=f16)
 
 
 def _run(gw, xs, chain, acquire=False, variant=0):
@@ -67,14 +67,19 @@ def _inputs(n, h, w, k, seed):
 # the trunk kernel addresses each 16-channel plane through its own resource (round 5)
 @pytest.mark.parametrize("n,h,w,blocks", [(2, 36, 52, 2), (1, 128, 128, 1), (16, 128, 128, 16), (4, 256, 256, 2),
                                           (4, 512, 512, 1), (1, 540, 960, 1), (10, 768, 768, 1)])
-def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks):
-    gw = _gw(blocks)
+@pytest.mark.parametrize("f16", [True, False], ids=["fp16", "bf16"])
+def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks, f16):
+    """fp16 storage (the inference default) runs the production trunk form only; the bf16 forms
+    (the training forward's storage) also sweep the tuning library's A/B forms."""
+    gw = _gw(blocks, f16=f16)
     xs = _inputs(n, h, w, 3, seed=3)
     refs = _run(gw, xs, chain=False)
     # variants 3 and 4 (32x32 tiles) need the 16-row-rounded height to be a multiple of 32
     variants = ((0, 9, 7, 8, 6, 5, 2, 1) + ((3, 4) if -(-h // 16) % 2 == 0 else ())) if TUNING_LIB else (0,)
     if os.environ.get("ISR_TEST_CHAIN_VARIANTS"):
         variants = tuple(int(v) for v in os.environ["ISR_TEST_CHAIN_VARIANTS"].split(","))
+    if f16:
+        variants = (0,)
     for variant in variants:
         for acquire in (False, True):
             for out, ref in zip(_run(gw, xs, chain=True, acquire=acquire, variant=variant), refs):

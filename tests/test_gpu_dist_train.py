@@ -172,10 +172,16 @@ def _delta_close(a, b, p0, rel_max, cos_min, what):
     print(f"{what}: worst parameter-change rel {worst[0]:.3e} (cos {worst[1]:.5f}) at {worst[2]}")
 
 
-@pytest.mark.parametrize("mode,bucket_mb", [("res", "0"), ("srgan", "0"), ("res", "8")])
-def test_two_rank_data_parallel_matches(mode, bucket_mb, tmp_path):
-    dp = _run(mode, 2, tmp_path / "dp", bucket_mb)
-    single = _run(mode, 1, tmp_path / "single")[0]
+# SRGAN under both enqueue orders of the two optimiser steps: the default (D's
+# step enqueued before G's) and ISR_TRAIN_G_FIRST=1 — the same arithmetic in another launch order,
+# so both must pass the same bars (tools/diag_dp_order.py taps: bitwise-identical per-step tensors
+# across the two orders, profiles/r06_diag_dp_order_s*.txt)
+@pytest.mark.parametrize("mode,bucket_mb,g_first", [("res", "0", False), ("srgan", "0", False),
+                                                    ("srgan", "0", True), ("res", "8", False)],
+                         ids=["res", "srgan", "srgan-g_first", "res-bucket8"])
+def test_two_rank_data_parallel_matches(mode, bucket_mb, g_first, tmp_path):
+    dp = _run(mode, 2, tmp_path / "dp", bucket_mb, g_first=g_first)
+    single = _run(mode, 1, tmp_path / "single", g_first=g_first)[0]
     # rank 1 started from other weights; after broadcast + 2 averaged steps both ranks agree bitwise
     np.testing.assert_array_equal(np.concatenate([v.ravel() for v in dp[0]["p0"].values()]),
                                   np.concatenate([v.ravel() for v in dp[1]["p0"].values()]))

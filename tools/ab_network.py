@@ -36,7 +36,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda")
     sd = synth_state_dict(models.ResNet(16, 0.2, scaleRate=4).state_dict(), seed=0)
-    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev)
+    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev, f16=False)
     lr, _ = synth_lr_batch(args.batch, args.lr_size, args.lr_size, seed=1234)
     x = normalize(lr).to(dev).contiguous()
     names = args.configs.split(",")

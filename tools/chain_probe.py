@@ -40,7 +40,7 @@ def main():
     lib = _lib.load()
     dev = torch.device("cuda")
     sd = synth_state_dict(models.ResNet(16, 0.2, scaleRate=4).state_dict(), seed=0)
-    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev)
+    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev, f16=False)
     lr, _ = synth_lr_batch(16, 128, 128, seed=1234)
     x = normalize(lr).to(dev).contiguous()
     plan = engine.GeneratorPlan(gw, 16, 128, 128, dev, False, False, (0.485, 0.456, 0.406),

@@ -4,7 +4,7 @@ from image_super_resolution_amd import engine, models
 from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_state_dict
 dev = torch.device("cuda")
 sd = synth_state_dict(models.ResNet(16, 0.2, scaleRate=4).state_dict(), seed=0)
-gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev)
+gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev, f16=False)
 lr, _ = synth_lr_batch(16, 128, 128, seed=1234)
 x = normalize(lr).to(dev).contiguous()
 mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)

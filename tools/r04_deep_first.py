@@ -17,7 +17,7 @@ def main():
     variant = int(sys.argv[5]) if len(sys.argv) > 5 else 4
     dev = torch.device("cuda")
     sd = synth_state_dict(models.ResNet(blocks, 0.2, scaleRate=4).state_dict(), seed=0)
-    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev)
+    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev, f16=False)
     xs = [normalize(synth_lr_batch(n, h, w, seed=3 + i, scale=4)[0]).to(dev).contiguous() for i in range(2)]
     mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
     ref_plan = engine.GeneratorPlan(gw, n, h, w, dev, False, False, mean, std, chain=False)

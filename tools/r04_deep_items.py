@@ -24,7 +24,7 @@ def main():
     engine.CHAIN_VARIANT = 4
     dev = torch.device("cuda")
     sd = synth_state_dict(models.ResNet(16, 0.2, scaleRate=4).state_dict(), seed=0)
-    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev)
+    gw = engine.pack_generator({k: v.to(dev) for k, v in sd.items()}, enchant=False, device=dev, f16=False)
     x = normalize(synth_lr_batch(16, 128, 128, seed=1234)[0]).to(dev).contiguous()
     plan = engine.GeneratorPlan(gw, 16, 128, 128, dev, False, False, (0.485, 0.456, 0.406),
                                 (0.229, 0.224, 0.225), chain=True)
