@@ -857,8 +857,6 @@ def step_guard_ptr(gen: nn.Module):
     group = _grad_group(gen)
     if group is None:
         return chain.guard_ptr if chain is not None else None
-    if chain is None and _os.environ.get("ISR_DIAG_ROUND5_GUARD", "0") == "1":
-        return None  # diagnostics only (tools/diag_dp_order.py): the round-5 chain-less behaviour
     g = plan.__dict__.get("_global_guard")
     if g is None:
         g = plan.__dict__["_global_guard"] = torch.zeros(2, dtype=torch.int32, device=_plan_device(plan))

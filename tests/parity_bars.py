@@ -7,14 +7,16 @@ generator's output (tanh space [-1, 1], peak 2) and on BT.601 luma with the 4-px
 (utils/datasets.py:159-166) — measured on the FLOAT output both paths round to uint8
 (TanhToArrayImage, utils/models.py:443-451).
 
-The uint8 images themselves carry the rounding of two paths that agree to ~66 dB in float: about
-9-10 % of the pixels land on the other side of a rounding boundary (+-1 LSB), independently of the
-HR image, which moves MSE(uint8, HR) by ~f1 * LSB^2 (f1 = the share of such pixels).  Against a
-model that is close to HR (the x2 weights reach 41 dB on dead-leaves crops: MSE ~5 LSB^2) that
-alone is ~0.04-0.08 dB, so the uint8 comparison is bounded by that rounding allowance plus the
-0.01 dB tolerance, and by its LSB distribution: > 1 LSB on < 0.1 % of the pixels, > 2 LSB on
-< 0.001 %, never more than 4 (the bf16 network's error tail: tests/diag_u8_outliers.py,
-profiles/r06_u8_outliers.json — spread over channels and positions, not on tile edges or borders)."""
+The uint8 images themselves carry the rounding of two paths that agree to 80-84 dB in float
+(fp16 storage, round 6; 66 dB in bf16): about 1-2 % of the pixels land on the other side of a
+rounding boundary (+-1 LSB; 9-10 % in bf16), independently of the HR image, which moves
+MSE(uint8, HR) by ~f1 * LSB^2 (f1 = the share of such pixels).  Against a model close to HR (the x2
+weights reach 41 dB on dead-leaves crops: MSE ~5 LSB^2) that alone is up to ~0.01 dB, so the uint8
+comparison is bounded by that rounding allowance plus the 0.01 dB tolerance, and by its LSB
+distribution: >= 1 LSB on < 5 % of the pixels, > 1 LSB on < 0.001 %, never more than 2 (measured
+on fp16: max 1 LSB everywhere, profiles/r06_fp16_parity.txt; the bf16 path's tail reached 3 LSB on
+46 of 3.1 M pixels, spread over channels and positions and not on tile edges or borders:
+tests/diag_u8_outliers.py, profiles/r06_u8_outliers.json)."""
 import math
 
 import torch
@@ -57,7 +59,7 @@ def u8_bars(got, ref, hr_u8, what):
     dp = abs(p_got - p_ref)
     print(f"{what} (uint8): {f1 * 100:.2f} % of pixels off by >= 1 LSB, {f2 * 100:.4f} % by >= 2, {f3 * 100:.5f} % by "
           f">= 3, max {d.max().item()}; dPSNR {dp:.5f} dB (rounding allowance {allow:.5f} dB)")
-    assert d.max().item() <= 4 and f2 < 1e-3 and f3 < 1e-5 and f1 < 0.2, (what, d.max().item(), f1, f2, f3)
+    assert d.max().item() <= 2 and f2 < 1e-5 and f1 < 0.05, (what, d.max().item(), f1, f2, f3)
     assert dp <= allow + TOL_DB, (what, dp, allow)
 
 

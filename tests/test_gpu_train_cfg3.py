@@ -175,7 +175,9 @@ def test_srgan_default_mode_step_vs_oracle():
       rel <= 3 % (the VGG feature bar of test_gpu_vgg.py);
     * every generator parameter gradient of the step vs autograd of the oracle generator fed the
       step's own upstream gradient dL/dSR (the VGG + discriminator input gradients, pinned by
-      test_gpu_vgg.py / test_gpu_disc.py): rel L2 <= 5e-2, cos >= 0.998 (test_gpu_train.py's bars)."""
+      test_gpu_vgg.py / test_gpu_disc.py): rel L2 <= max(5e-2, 1.3 x torch bf16 autocast's own
+      rel L2 + 0.02) (test_gpu_train.py's bar, widened as test_gpu_denoise.py's for BatchNorm
+      graphs), cos >= 0.998."""
     import copy
 
     torch.manual_seed(0)
@@ -234,15 +236,27 @@ def test_srgan_default_mode_step_vs_oracle():
     assert abs(adversarial - a_ref.item()) <= 3e-2 * abs(a_ref.item()) + 1e-3, (adversarial, a_ref.item())
     assert abs(perceptual - (content + 1e-3 * adversarial)) <= 1e-5 * abs(perceptual) + 1e-7
 
-    # generator gradients for the step's own upstream gradient
+    # generator gradients for the step's own upstream gradient; the yardstick beside the fixed bar is
+    # the error torch's own bf16 autocast makes on the same graph (the reference trains under
+    # autocast, train.py:54; as tests/test_gpu_denoise.py): train-mode BatchNorm subtracts batch
+    # means in its backward, so the BN generator's gradients carry more relative rounding error
+    # than the BN-free EResNet's (test_gpu_train.py)
     sr_ref.backward(gy)
+    sd_amp = {k: v.detach().clone().to(DEV) for k, v in sd_g.items()}
+    p_amp = {k: v.requires_grad_(True) for k, v in sd_amp.items() if k in pnames}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        sr_amp = R.generator(sd_amp, lr.float(), num_blocks=16, scale=2, enchant=False, train_bn=True)
+    sr_amp.float().backward(gy.to(DEV))
     names = [k for k, _ in gen.named_parameters()]
     worst = []
     for name, g in zip(names, taps["g_grad"]):
-        r = params[name[len("res_net."):]].grad
+        key = name[len("res_net."):]
+        r = params[key].grad
         rel = ((g - r).norm() / r.norm().clamp_min(1e-12)).item()
+        rel_amp = ((p_amp[key].grad.cpu() - r).norm() / r.norm().clamp_min(1e-12)).item()
         cos = F.cosine_similarity(g.flatten().double(), r.flatten().double(), dim=0).item()
-        worst.append((rel, cos, name))
-        assert rel <= 5e-2 and cos >= 0.998, f"{name}: rel {rel:.3e} cos {cos:.5f}"
+        worst.append((round(rel, 4), round(rel_amp, 4), round(cos, 5), name))
+        assert rel <= max(5e-2, 1.3 * rel_amp + 0.02) and cos >= 0.998, \
+            f"{name}: rel {rel:.3e} (bf16 autocast {rel_amp:.3e}) cos {cos:.5f}"
     worst.sort(reverse=True)
-    print("default SRGAN mode, worst generator gradients vs oracle autograd:", worst[:3])
+    print("default SRGAN mode, worst generator gradients vs oracle autograd (rel, autocast rel, cos):", worst[:4])

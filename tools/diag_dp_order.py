@@ -52,11 +52,10 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--repeats", type=int, default=2)
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "diag_dp_order.txt"))
-    ap.add_argument("--round5-guard", action="store_true",
-                    help="chain-less ranks skip the global guard's all-reduce (the round-5 code path)")
     a = ap.parse_args()
-    import os
-    os.environ["ISR_DIAG_ROUND5_GUARD"] = "1" if a.round5_guard else "0"  # inherited by the spawned ranks
+    # (a --round5-guard option re-created the round-5 chain-less guard path for one run,
+    # profiles/r06_diag_dp_order_s2_r5guard.txt: identical to the current path at every tap, so
+    # the knob was removed from train_engine)
     import test_gpu_dist_train as T
 
     runs = {}
