@@ -91,7 +91,7 @@ def parse():
                     help="tiles the CPU baseline runs one by one (the first is the warm-up; all of them are the "
                          "parity reference)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r05")  # PMC traffic file (profiles/<round>_pmc_traffic.json)
+    ap.add_argument("--round", default="r06")  # PMC traffic file (profiles/<round>_pmc_traffic.json)
     ap.add_argument("--weights", default=str(ROOT / "tests" / "golden" / "trained_resnet_x4.safetensors"),
                     help="generator state_dict (default: the committed trained ResNet(16, 0.2, x4)); "
                          "'synth' = the seeded synthetic weights of earlier rounds")

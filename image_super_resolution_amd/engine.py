@@ -168,6 +168,10 @@ class GeneratorPlan:
         if chain_acquire is None:
             chain_acquire = CHAIN_ACQUIRE
         self.key = (n, h, w, str(device), x_u8, out_u8, tuple(mean), tuple(std))
+        # the descriptors hold raw pointers into gw's packed weights: the plan keeps gw alive (a plan
+        # that outlived its weights read whatever reused that memory — found by tools/ab_storage.py,
+        # whose bf16 plan's weights were freed and refilled by the fp16 packs built after it)
+        self.gw = gw
         bufs = GeneratorBuffers(n, h, w, len(gw.scalers), device, gw.dtype)
         self.bufs = bufs
         feat = bufs.feat

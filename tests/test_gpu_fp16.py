@@ -215,3 +215,29 @@ def test_trained_x2_generator_fp16_vs_bf16_vs_oracle():
           f"bf16 {res[False][0]:.2f} dB (dPSNR {res[False][1]:.5f})")
     assert res[True][0] >= 70.0 and res[True][0] >= res[False][0] + 10.0, res
     assert res[True][1] <= 0.002, res
+
+
+@torch.no_grad()
+def test_plan_keeps_its_packed_weights_alive():
+    """A GeneratorPlan's descriptors point into its GeneratorWeights' packed tensors: the plan must
+    keep them alive.  Build a bf16 plan, drop every other reference to its weights, pack fp16
+    weights of the same shapes (which would reuse the freed blocks) and rerun: the output is
+    unchanged (round 6: tools/ab_storage.py's bf16 plan ran on fp16 bits after exactly this)."""
+    import gc
+
+    from image_super_resolution_amd import engine, models
+    from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_state_dict
+    sd = {k: v.to(DEV) for k, v in synth_state_dict(models.ResNet(2, 0.2, scaleRate=4).state_dict(), 0).items()}
+    x = normalize(synth_lr_batch(2, 32, 32, seed=1)[0]).to(DEV).contiguous()
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    plan = engine.GeneratorPlan(engine.pack_generator(sd, enchant=False, device=DEV, f16=False), 2, 32, 32,
+                                torch.device(DEV), False, False, mean, std, chain=True)
+    y0 = torch.empty(plan.out_shape, device=DEV)
+    plan.run(x, y0)
+    torch.cuda.synchronize()
+    gc.collect()
+    others = [engine.pack_generator(sd, enchant=False, device=DEV, f16=True) for _ in range(2)]
+    y1 = torch.empty(plan.out_shape, device=DEV)
+    plan.run(x, y1)
+    plan.verify()
+    assert others and torch.isfinite(y1).all() and torch.equal(y0, y1)

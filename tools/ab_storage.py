@@ -25,11 +25,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--weights", default=str(Path(__file__).resolve().parents[1] / "tests" / "golden" /
+                                             "trained_resnet_x4.safetensors"), help="'synth' or a state_dict file")
     args = ap.parse_args()
     dev = torch.device("cuda")
-    sd = synth_state_dict(models.ResNet(16, 0.2, scaleRate=4).state_dict(), seed=0)
-    lr, _ = synth_lr_batch(16, 128, 128, seed=1234)
-    x = normalize(lr).to(dev).contiguous()
+    if args.weights == "synth":
+        sd = synth_state_dict(models.ResNet(16, 0.2, scaleRate=4).state_dict(), seed=0)
+        lr, _ = synth_lr_batch(16, 128, 128, seed=1234)
+        x = normalize(lr).to(dev).contiguous()
+    else:  # bench.py's default workload: the trained weights on held-out tiles
+        from image_super_resolution_amd import checkpoint
+        from image_super_resolution_amd.weights import HELDOUT_SEED, heldout_tiles
+        sd = checkpoint.load_module_state(args.weights)
+        x = heldout_tiles(16, 128, 4, seed=HELDOUT_SEED)[0].to(dev).contiguous()
     mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
     runs = {}
     for name, f16 in (("bf16", False), ("fp16", True)):
@@ -55,8 +63,10 @@ def main():
         p.verify()
     d = (runs["fp16"][1] - runs["bf16"][1]).abs().max().item()
     for k in runs:
-        print(json.dumps({"storage": k, "ms_median": round(statistics.median(t[k]), 4),
-                          "ms_min": round(min(t[k]), 4), "rounds": t[k] and len(t[k]),
+        o = runs[k][1]
+        print(json.dumps({"storage": k, "weights": Path(args.weights).name, "ms_median": round(statistics.median(t[k]), 4),
+                          "ms_min": round(min(t[k]), 4), "rounds": len(t[k]),
+                          "nonfinite_outputs": int((~torch.isfinite(o)).sum().item()),
                           "max_abs_diff_fp16_vs_bf16": round(d, 5)}), flush=True)
 
 
