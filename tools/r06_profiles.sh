@@ -11,3 +11,5 @@ for b in 1 2; do
   timeout -k 10 240 python -u tools/bench_video.py --frames 24 --batch $b >> gpurun_out/r06/video_bench.jsonl 2>> gpurun_out/r06/video_err.txt || exit 1
 done
 timeout -k 10 300 python -u tools/bench_still.py --shard blocks > gpurun_out/r06/still_blocks.json 2> gpurun_out/r06/still_err.txt
+timeout -k 10 300 python -u -m pytest -v -s --timeout 300 --timeout-method thread tests/test_gpu_train_cfg3.py -k default_mode > gpurun_out/r06/t8_cfg3.txt 2>&1
+echo "cfg3 default-mode test rc=$?"
