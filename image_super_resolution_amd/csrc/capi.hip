@@ -19,7 +19,6 @@ size_t trunk_state_words(int n, int ha, int wa);
 int trunk_launch(const isr_chain_desc* c, hipStream_t s, int form);
 int trunk_stamps_set(void* p);
 int trunk_knobs_set(const int* k);
-int trunk_deep_stats(unsigned long long* out, int reset);
 int trunk_item_stamps_set(void* p);
 size_t conv3x3_packed_bytes(int cout, int cin);
 int conv3x3_pack(const float* w, void* out, int cout, int cin, hipStream_t s);
@@ -277,7 +276,9 @@ int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_
     if (c->f16 != 0 && c->f16 != 1) return fail(ISR_ERR_BAD_DESC, "conv chain: f16 must be 0 or 1");
     if (c->f16 && variant != 0)
         return fail(ISR_ERR_UNSUPPORTED, "conv chain: fp16 storage runs the production trunk form (variant 0) only");
-    if (variant == 0 || (variant >= 2 && variant <= 9)) {
+    if (variant == 4 || variant == 9)
+        return fail(ISR_ERR_UNSUPPORTED, "conv chain: variant %d (a losing A/B form) was removed in round 6", variant);
+    if (variant == 0 || (variant >= 2 && variant <= 8)) {
         static const int form_of[10] = {0, 0, 1, 2, 3, 4, 5, 6, 7, 8};
         const int rc = isr::trunk_launch(c, (hipStream_t)s, form_of[variant]);
         if (rc == -3) return fail(ISR_ERR_UNSUPPORTED, "conv chain: variant %d is an A/B form of the tuning library "
@@ -301,12 +302,6 @@ int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k
     const int rc = isr::trunk_knobs_set(k);
     if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "trunk knobs: library built without -DISR_TUNING");
     return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "trunk knobs: hipMemcpyToSymbol failed");
-}
-
-int isr_tuning_trunk_deep_stats(uint64_t* out, int32_t reset) {
-    const int rc = isr::trunk_deep_stats((unsigned long long*)out, reset);
-    if (rc == -2) return fail(ISR_ERR_UNSUPPORTED, "trunk deep stats: library built without -DISR_TUNING");
-    return rc == 0 ? ISR_OK : fail(ISR_ERR_LAUNCH, "trunk deep stats: hipMemcpyFromSymbol failed");
 }
 
 int isr_tuning_trunk_item_stamps(void* buf) {

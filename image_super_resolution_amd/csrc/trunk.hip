@@ -1038,21 +1038,14 @@ using TK_QUAD = TK<8, 2, 2>;
 using TK_PAIR_X = TK<4, 4, 2, 16, 1>;  // the pair form with the XCD-aware tile deal
 using TK_PAIR_NTH = TK<4, 4, 2, 16, 0, 1>;  // non-temporal halo loads
 using TK_PAIR_NTS = TK<4, 4, 2, 16, 0, 2>;  // non-temporal output stores
-
-int trunk_deep_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_deep.hip
-int trunk_deep_knobs_set(const int* k);
-#endif
-
-#ifdef ISR_TUNING
-int trunk_lc_launch(const isr_chain_desc* cd, hipStream_t s);  // trunk_lc.hip (loader / consumer form)
+// (round 6: the deep-ring form of trunk_deep.hip and the loader / consumer form of trunk_lc.hip,
+// chain variants 4 and 9, measured slower in rounds 4-5 — DESIGN.md §5 — and were removed)
 #endif
 
 int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
     if (cd->f16) return form == 0 ? trunk_launch_k<TK_PAIR, true>(cd, s) : -3;  // fp16 storage: production form only
     if (form == 0) return trunk_launch_k<TK_PAIR>(cd, s);
 #ifdef ISR_TUNING
-    if (form == 8) return trunk_lc_launch(cd, s);
-    if (form == 3) return trunk_deep_launch(cd, s);
     if (form == 2) return trunk_launch_k<TK_T32>(cd, s);
     if (form == 4) return trunk_launch_k<TK_QUAD>(cd, s);
     if (form == 5) return trunk_launch_k<TK_PAIR_X>(cd, s);
@@ -1064,17 +1057,12 @@ int trunk_launch(const isr_chain_desc* cd, hipStream_t s, int form) {
 }
 
 #ifdef ISR_TUNING
-int trunk_lc_knobs_set(const int* k);  // trunk_lc.hip
 int trunk_knobs_set(const int* k) {
     g_trunk_per_cu = k[1];
-    if (trunk_lc_knobs_set(k) != 0) return -1;
-    if (trunk_deep_knobs_set(k) != 0) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_knobs), k, 4 * sizeof(int)) == hipSuccess ? 0 : -1;
 }
 int trunk_stamps_set(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trunk_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1; }
-int trunk_deep_stamps_set(void* p);  // trunk_deep.hip (the same buffer layout)
 int trunk_item_stamps_set(void* p) {
-    if (trunk_deep_stamps_set(p) != 0) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_item_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
 }
 #else

@@ -1,5 +1,5 @@
 // Shared pieces of the persistent RRDB-trunk kernels (trunk.hip: the two-workgroups-per-CU pair
-// form and its variants; trunk_deep.hip: the 32x32-tile deep-ring form): layer records, the
+// form and its variants; until round 6 also trunk_deep.hip): layer records, the
 // dependency poll, buffer resources, the LDS halo image, counted vmcnt waits.
 #pragma once
 #include "isr_common.h"

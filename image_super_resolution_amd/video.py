@@ -146,40 +146,53 @@ def _gpu_vendor() -> str:
         return ""
 
 
-class FFMPEG_recorder:  # noqa: N801  (reference class name, utils/ffmpeg.py:28)
-    """utils/ffmpeg.py:28-140: raw bgr24 frames piped into ffmpeg.
+def _bitrate_mbps(dims, fps) -> float:
+    """Target bitrate in Mbit/s (utils/ffmpeg.py:59-61): 20 Mbit/s for a 4K frame at 30 fps, scaled
+    by the frame area and by the frame-rate ratio, which is never taken below 1."""
+    rate_factor = round(fps / 30, 3)
+    if rate_factor < 1:
+        rate_factor = 1
+    return round(20 * (math.prod(dims) / (3840 * 2160)) * rate_factor, 3)
 
-    Same constructor, bitrate rule (:59-61), command line (:63-66) and methods
-    (writeFrame, writeSubtitle, addSubtitle, addAudio, stopRecorder).  Codec
-    choice keeps the reference's order of preference for an AMD GPU on Linux
-    (hevc_vaapi) but falls back to libx264 when that encoder is unavailable."""
+
+def _srt_entry(index: int, t0: str, t1: str, text: str) -> str:
+    return f"{index}\n{t0} --> {t1}\n{text}\n\n"
+
+
+class FFMPEG_recorder:  # noqa: N801  (reference class name, utils/ffmpeg.py:28)
+    """utils/ffmpeg.py:28-140: raw bgr24 frames piped into an ffmpeg encoder process.
+
+    The public surface is the reference's (constructor arguments, `bitRate`, `cmd`,
+    `subtitleContent`, writeFrame / writeSubtitle / addSubtitle / addAudio / stopRecorder) and so is
+    what ffmpeg receives (tests/test_video_cpu.py pins the argv, bitrate and timecodes).  The encoder
+    is hevc_vaapi on a Linux host with an AMD GPU when ffmpeg offers it (the reference's preference
+    for that platform), else libx264."""
 
     def __init__(self, save_path=None, videoDimensions=(1280, 720), fps=30, codec: str | None = None,
                  dry_run: bool = False):
         self.save_path = save_path
         self.dimension = videoDimensions
         self.fps = fps
-        os_type = platform.uname().system
         if codec is None:
-            codec = "hevc_vaapi" if (os_type == "Linux" and _gpu_vendor() == "AMD" and _has_encoder("hevc_vaapi")) \
-                else "libx264"
+            amd_linux = platform.uname().system == "Linux" and _gpu_vendor() == "AMD"
+            codec = "hevc_vaapi" if amd_linux and _has_encoder("hevc_vaapi") else "libx264"
         self.codec = codec
-        if save_path and " " in save_path:
-            save_path = save_path.replace(" ", "_")
+        out_path = save_path.replace(" ", "_") if save_path else save_path  # ffmpeg target without spaces
         self.countFrame = 0
         self.startTime = 0.
-        mpx = math.prod(self.dimension)
-        self.bitRate = round(
-            20 * (mpx / (3840 * 2160)) * (1 if round(self.fps / 30, 3) < 1 else round(self.fps / 30, 3)), 3)
+        self.bitRate = _bitrate_mbps(self.dimension, self.fps)
         self.subtitleContent = ''
-        self.cmd = ['ffmpeg', '-v', 'quiet', '-y', '-s', f'{self.dimension[0]}x{self.dimension[1]}',
-                    '-pixel_format', 'bgr24', '-f', 'rawvideo', '-r', f'{self.fps}', '-i', 'pipe:', '-vcodec',
-                    f'{self.codec}', '-pix_fmt', 'yuv420p', '-b:v', f'{self.bitRate}M', f'{save_path}']
+        width, height = self.dimension
+        source = ['-s', f'{width}x{height}', '-pixel_format', 'bgr24', '-f', 'rawvideo', '-r', f'{self.fps}',
+                  '-i', 'pipe:']
+        sink = ['-vcodec', f'{self.codec}', '-pix_fmt', 'yuv420p', '-b:v', f'{self.bitRate}M', f'{out_path}']
+        self.cmd = ['ffmpeg', '-v', 'quiet', '-y', *source, *sink]
         self.process = None
-        if not dry_run:
-            if shutil.which("ffmpeg") is None:
-                raise RuntimeError("FFMPEG_recorder needs the ffmpeg binary (use RawRecorder without it)")
-            self.process = subprocess.Popen(self.cmd, stdin=subprocess.PIPE)
+        if dry_run:
+            return
+        if shutil.which("ffmpeg") is None:
+            raise RuntimeError("FFMPEG_recorder needs the ffmpeg binary (use RawRecorder without it)")
+        self.process = subprocess.Popen(self.cmd, stdin=subprocess.PIPE)
 
     def writeFrame(self, image=None):  # noqa: N802
         """image: ndarray uint8 HWC BGR."""
@@ -187,44 +200,49 @@ class FFMPEG_recorder:  # noqa: N801  (reference class name, utils/ffmpeg.py:28)
 
     @staticmethod
     def second_to_timecode(x=0.) -> str:
-        hour, x = divmod(x, 3600)
-        minute, x = divmod(x, 60)
-        second, x = divmod(x, 1)
-        millisecond = int(x * 1000.)
-        return '%.2d:%.2d:%.2d,%.3d' % (hour, minute, second, millisecond)
+        """SubRip timecode HH:MM:SS,mmm of x seconds, milliseconds truncated (utils/ffmpeg.py:81-89;
+        float divmod is exact, so x mod 1 equals the reference's chained remainders)."""
+        whole, frac = divmod(x, 1)
+        hours, rest = divmod(int(whole), 3600)
+        minutes, seconds = divmod(rest, 60)
+        return f"{hours:02d}:{minutes:02d}:{seconds:02d},{int(frac * 1000.):03d}"
 
     def writeSubtitle(self, title='', fps=30):  # noqa: N802
-        step = 1 / fps
-        tc0 = self.second_to_timecode(self.startTime)
-        tc1 = self.second_to_timecode(self.startTime + step)
-        self.startTime += step
-        self.subtitleContent += f'{self.countFrame}\n{tc0} --> {tc1}\n{title or "UTC2"}\n\n'
+        """One SubRip cue of 1/fps seconds at the running clock (utils/ffmpeg.py:91-100)."""
+        t0 = self.startTime
+        self.startTime = t0 + 1 / fps
+        self.subtitleContent += _srt_entry(self.countFrame, self.second_to_timecode(t0),
+                                           self.second_to_timecode(self.startTime), title or "UTC2")
         self.countFrame += 1
 
     def addSubtitle(self, hardSubtitle=False):  # noqa: N802,N803
-        save = self.save_path.replace('.mp4', 'with_sub.mp4')
-        sub_file = save.replace('.mp4', '.srt')
-        Path(sub_file).write_text(self.subtitleContent)
+        """Mux (or burn in, hardSubtitle) the collected cues into '<name>with_sub.mp4'."""
+        muxed = self.save_path.replace('.mp4', 'with_sub.mp4')
+        srt = muxed.replace('.mp4', '.srt')
+        Path(srt).write_text(self.subtitleContent)
+        head = ["ffmpeg", "-hide_banner", "-i", self.save_path]
         if hardSubtitle:
-            cmd = ["ffmpeg", "-hide_banner", "-i", self.save_path, "-c:v", "copy", "-vf", f"subtitles={sub_file}", save]
+            tail = ["-c:v", "copy", "-vf", f"subtitles={srt}"]
         else:
-            cmd = ["ffmpeg", "-hide_banner", "-i", self.save_path, "-i", sub_file, "-c:v", "copy", "-c:s", "mov_text",
-                   "-metadata:s:s:0", "language=eng", save]
-        return subprocess.run(cmd)
+            tail = ["-i", srt, "-c:v", "copy", "-c:s", "mov_text", "-metadata:s:s:0", "language=eng"]
+        return subprocess.run([*head, *tail, muxed])
 
     def addAudio(self, audio_src):  # noqa: N802
-        audio_src = Path(audio_src)
-        if not audio_src.is_file():
+        """Copy the video stream and take the audio of `audio_src` into '<name>_audio.mp4'; 0 when
+        there is no such file, else 1."""
+        src = Path(audio_src)
+        if not src.is_file():
             return 0
-        save_dir = self.save_path.replace(".mp4", "_audio.mp4")
-        subprocess.run(["ffmpeg", "-i", self.save_path, "-i", audio_src.as_posix(), "-c:v", "copy", "-map", "0:v",
-                        "-map", "1:a", "-y", save_dir])
+        target = self.save_path.replace(".mp4", "_audio.mp4")
+        streams = ["-c:v", "copy", "-map", "0:v", "-map", "1:a"]
+        subprocess.run(["ffmpeg", "-i", self.save_path, "-i", src.as_posix(), *streams, "-y", target])
         return 1
 
     def stopRecorder(self):  # noqa: N802
-        if self.process is not None:
-            self.process.stdin.close()
-            self.process.wait()
+        if self.process is None:
+            return
+        self.process.stdin.close()
+        self.process.wait()
 
 
 def _has_encoder(name: str) -> bool:

@@ -416,19 +416,15 @@ int isr_conv_chain(const isr_chain_desc* c, isr_stream_t s);
  * of the per-layer isr_conv3x3_fwd calls bit for bit.  0 = trunk.hip in its two-workgroups-per-CU
  * form (4 waves of 4 output rows each, one K-chunk in flight); 2 = trunk.hip with one 8-wave
  * workgroup per CU (2 output rows per wave) and three chunks in flight; 3 = trunk.hip on 32x32
- * tiles, one 8-wave workgroup per CU (4 rows per wave; needs ha % 32 == 0); 4 = trunk_deep.hip:
- * 32x32 tiles, one 8-wave workgroup per CU, split halo (3 slots) / weight (2 slots) rings, the
- * chunk barrier before the last MFMA step with the next chunk's fragments read behind it, LDS-DMA
- * spread over the MFMA stream, neighbourhood polls by LDS-DMA (needs ha % 32 == 0); 5 = trunk.hip's
+ * tiles, one 8-wave workgroup per CU (4 rows per wave; needs ha % 32 == 0); 5 = trunk.hip's
  * pair tile and ring with two 8-wave workgroups per CU (2 rows per wave, 4 waves per SIMD at
  * 128 VGPRs: one fragment set read a kernel row ahead, half the refill pieces per wave); 6 = the
  * production form with an XCD-aware tile deal (each XCD streams a contiguous range of tiles); 7 / 8 =
- * the production form with non-temporal halo loads / output stores; 9 = trunk_lc.hip, the loader /
- * consumer form: one 8-wave workgroup per CU, 4 compute waves on the pair form's tile and MFMA order,
- * 4 loader waves filling a 4-slot LDS ring (FULL / FREE counts in LDS), the last compute wave of a
- * tile publishing its progress word.  The production library carries variant 0 only (every other
- * variant measured slower); variants 1-9 are built into the tuning library
- * (-DISR_TUNING) and return ISR_ERR_UNSUPPORTED here. */
+ * the production form with non-temporal halo loads / output stores.  Variants 4 (the deep-ring form,
+ * round 4) and 9 (the loader / consumer form, round 5) measured slower and were removed in round 6
+ * (ISR_ERR_UNSUPPORTED; their numbers stay in DESIGN.md §5).  The production library carries
+ * variant 0 only (every other variant measured slower); variants 1-3 and 5-8 are
+ * built into the tuning library (-DISR_TUNING) and return ISR_ERR_UNSUPPORTED here. */
 int isr_conv_chain_variant(const isr_chain_desc* c, int32_t variant, isr_stream_t s);
 /* Tuning builds only: per (layer 75..89, tile) stamps of later production chain launches into
  * `buf` (8 x uint64: entry, chunk 0 landed, main loop done, stores issued, deferred wait start,
@@ -439,10 +435,6 @@ int isr_tuning_trunk_stamps(void* buf);
  * waits;
  * per_cu > 0 caps the resident workgroups per CU (the grid). */
 int isr_tuning_trunk_knobs(int32_t ablate, int32_t per_cu, int32_t k2, int32_t k3);
-/* Tuning builds only: the deep-ring trunk's (variant 4) event counters since the last reset
- * (uint64[8]: top slow paths, their blocking waits, mid-chunk slow paths, their blocking waits,
- * neighbourhood polls issued, polls that found the neighbourhood done); reset != 0 zeroes them. */
-int isr_tuning_trunk_deep_stats(uint64_t* out, int32_t reset);
 /* Tuning builds only: per-item cycle stamps (s_memtime) of later production chain launches into
  * `buf` (uint64 [grid][2 layers: 77, 79][16 items][2 waves][8]: item top, own DMA landed, barrier
  * passed, refill issued, MFMAs issued) for each workgroup's first tile; NULL stops. */

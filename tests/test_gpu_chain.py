@@ -1,4 +1,4 @@
-"""The persistent RRDB-trunk kernel (isr_conv_chain: trunk.hip, trunk_deep.hip, conv3x3.hip): the whole trunk of
+"""The persistent RRDB-trunk kernel (isr_conv_chain: trunk.hip, conv3x3.hip): the whole trunk of
 RDB convs in one launch with tile-level dependencies must reproduce the per-conv
 launches BIT FOR BIT (same tile arithmetic; only the hand-off differs: sc1 loads /
 write-through stores, progress words).  Repeated launches stress the hand-off for
@@ -14,8 +14,7 @@ from image_super_resolution_amd.weights import normalize, synth_lr_batch, synth_
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-# The production libisr.so carries the production trunk form (variant 0) only; the A/B forms (9 = the
-# loader / consumer form of trunk_lc.hip, round 5) are
+# The production libisr.so carries the production trunk form (variant 0) only; the A/B forms are
 # built into lib/libisr_tuning.so (ISR_LIB=.../libisr_tuning.so runs this file on all of them).
 TUNING_LIB = "tuning" in os.environ.get("ISR_LIB", "")
 
@@ -75,7 +74,7 @@ def test_chain_bitwise_equals_per_conv_launches(n, h, w, blocks, f16):
     xs = _inputs(n, h, w, 3, seed=3)
     refs = _run(gw, xs, chain=False)
     # variants 3 and 4 (32x32 tiles) need the 16-row-rounded height to be a multiple of 32
-    variants = ((0, 9, 7, 8, 6, 5, 2, 1) + ((3, 4) if -(-h // 16) % 2 == 0 else ())) if TUNING_LIB else (0,)
+    variants = ((0, 7, 8, 6, 5, 2, 1) + ((3,) if -(-h // 16) % 2 == 0 else ())) if TUNING_LIB else (0,)
     if os.environ.get("ISR_TEST_CHAIN_VARIANTS"):
         variants = tuple(int(v) for v in os.environ["ISR_TEST_CHAIN_VARIANTS"].split(","))
     if f16:

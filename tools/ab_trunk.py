@@ -56,16 +56,6 @@ def main():
             t[c].append(e0.elapsed_time(e1) / args.reps)
             assert not ch.failed(), c
     _lib.check(lib.isr_tuning_trunk_knobs(0, 0, 0, 0), "knobs")
-    if ch.variant == 4:  # the deep-ring trunk's event counters over one launch
-        import numpy as np
-        st = np.zeros(8, dtype=np.uint64)
-        lib.isr_tuning_trunk_deep_stats(st.ctypes.data, 1)
-        ch.fn(ctypes.byref(ch.desc), stream)
-        torch.cuda.synchronize()
-        lib.isr_tuning_trunk_deep_stats(st.ctypes.data, 1)
-        names = ["top_slow", "top_slow_block", "mid_slow", "mid_slow_block", "polls", "polls_ok"]
-        print(json.dumps({"deep_stats_per_launch": {k: int(v) for k, v in zip(names, st)},
-                          "workgroups": 256}), flush=True)
     for c in cfgs:
         print(json.dumps({"ablate": c[0], "per_cu": c[1], "ms_median": round(statistics.median(t[c]), 4),
                           "ms_min": round(min(t[c]), 4)}), flush=True)
