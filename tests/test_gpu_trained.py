@@ -97,6 +97,7 @@ def test_trained_u8_model(case):
     diff = (y.int() - ref.int()).abs()
     f1, f2 = (diff > 0).float().mean().item(), (diff > 1).float().mean().item()
     print(f"uint8: {f1 * 100:.3f} % of pixels differ by 1 LSB or more, {f2 * 100:.4f} % by 2, max {diff.max().item()}")
-    # ~1e-3 RMS on [-1, 1] is ~0.13 LSB: a pixel within that of a rounding boundary flips by one;
-    # the error's tail (a few 1e-5 of the pixels) reaches a second LSB
-    assert diff.max().item() <= 2 and f2 < 1e-3 and f1 < 0.2
+    # fp16 storage (round 6): ~1.2e-4 RMS on [-1, 1] is ~0.016 LSB, so only pixels that close to a
+    # rounding boundary flip, by one — the round-4 bar (<= 1 LSB) again.  (bf16, ~1e-3 RMS: ~9 % of
+    # pixels at 1 LSB and a tail of a few 1e-5 at 2 LSB, profiles/r06_u8_outliers.json.)
+    assert diff.max().item() <= 1 and f1 < 0.05
