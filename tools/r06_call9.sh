@@ -15,3 +15,4 @@ step() {  # step <seconds> <log> <cmd...>
 step 900 t9_suite.txt python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/
 step 300 t9_smoke.txt python -u -c "import __graft_entry__ as g; g.smoke()"
 ISR_LIB=$PWD/image_super_resolution_amd/lib/libisr_tuning.so step 400 t9_chain_tuning.txt python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_gpu_chain.py -k bitwise
+ISR_LIB=$PWD/image_super_resolution_amd/lib/libisr_tuning.so step 300 t9_ab_scaler.txt python -u tools/ab_scaler.py --variants 0,1,2,3,8,9 --rounds 7 --steps 5
