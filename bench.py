@@ -488,7 +488,9 @@ def main():
                        "global_batch": n * world, "per_gpu_batch": n, "lr_size": hw, "scale": S,
                        "parallelism": f"dp{world} (independent tile shards)",
                        "streams_per_gpu": n_streams, "hip_graph": not args.no_graph,
-                       "trunk": "persistent chain kernel" if chained else "one launch per conv"},
+                       "trunk": "persistent chain kernel" if chained else "one launch per conv",
+                       "storage": ("fp16" if gw.dtype == torch.float16 else "bf16")
+                                  + " activations and packed weights, fp32 accumulation"},
             "roofline": kernels.get("chain", kernels["growth"]),
             "roofline_kernels": kernels,
             "model_roofline": model_roofline,

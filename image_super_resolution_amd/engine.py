@@ -317,6 +317,11 @@ class ConvChain:
         if self.variant in (3, 4) and grid.ha % 32:
             raise ValueError(f"conv chain: variant {self.variant} (32x32 trunk tiles) needs the padded height "
                              "a multiple of 32")
+        if self.variant == 1 and grid.t.numel() * grid.t.element_size() >= 2 ** 31:
+            # the round-2 kernel's hand-off loads / stores address a whole buffer through one
+            # descriptor with 32-bit offsets (isr_common.h rsrc_of)
+            raise ValueError("conv chain: variant 1 (the round-2 kernel) needs every activation buffer below "
+                             "2 GiB")
         if 2 in kinds and self.variant in (1, 4):
             raise ValueError(f"conv chain: variant {self.variant} has no masked (kind 2) layers")
         if self.variant == 4 and any(d.cin % 32 or (k == 1 and (not d.r1.data or d.cin < 96))
