@@ -25,7 +25,8 @@ for r in rows:          # training leg's bf16 trunk are different kernels of one
     by[(r["Kernel_Name"], int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))].append(
         int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 out = [{"kernel": k, "blocks": b, "dispatches": len(v), "avg_us": round(sum(v) / len(v) / 1e3, 3),
-        "min_us": round(min(v) / 1e3, 3),
+        "min_us": round(min(v) / 1e3, 3), "median_us": round(sorted(v)[len(v) // 2] / 1e3, 3),
+        "durations_us_in_launch_order": [round(x / 1e3, 1) for x in v],
         "role": "persistent trunk kernel (trunk.hip), one launch per forward"
                 + (" (inference, fp16 storage)" if ", true>" in k else " (bf16: the bench's training leg)")}
        for (k, b), v in sorted(by.items())]
