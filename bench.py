@@ -151,6 +151,29 @@ def time_family(plan, tags, stream, sp, rounds=5):
     return statistics.median(res), [t for _, _, t in launches]
 
 
+def time_in_forward(plan, x, out, tags, steps):
+    """Mean per-launch ms of the launches tagged in `tags` INSIDE whole forwards: `steps` eager
+    forwards of the production plan back to back (no synchronisation between them, so the chip
+    stays in the sustained state of the timed region), each tagged launch bracketed by HIP events
+    on its launch stream (GeneratorPlan.run's `around` hook).  Isolated launches with an idle gap
+    before each run at a boosted clock (round 6: 5.0-5.3 ms for the fp16 trunk against ~6.0 ms
+    sustained, profiles/r06_trunk_dispatches.json), so they overstate a kernel's rate."""
+    evs = []
+
+    def around(tag):
+        if tag not in tags:
+            return None
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        evs.append(e)
+        return e
+
+    for _ in range(steps):
+        plan.run(x, out, around=around)
+    torch.cuda.synchronize()
+    ts = [a.elapsed_time(b) for a, b in evs]
+    return statistics.mean(ts), ts
+
+
 def parity_report(ref_cpu, gpu: torch.Tensor, ref: torch.Tensor, hr01: torch.Tensor, weights_desc: str) -> dict:
     """North-star parity over every tile the CPU reference ran: |PSNR(GPU, HR) - PSNR(ref, HR)| on
     the [-1, 1] output (peak 2) and on BT.601 luma with the 4-px border crop (utils/datasets.py:
@@ -365,8 +388,8 @@ def main():
     hr_px = n * (hw * S) * (hw * S)
     mpix_s = world * hr_px * args.steps / elapsed / 1e6
     # Per-kernel roofline, after the timed region.  The production forward's dominant kernel
-    # is the persistent trunk kernel (isr_conv_chain, all 240 RDB convs): its launch replayed
-    # back to back on the launch stream between HIP events.  The per-conv kernels (used by the
+    # is the persistent trunk kernel (isr_conv_chain, all 240 RDB convs): timed inside whole
+    # forwards run back to back (time_in_forward; its isolated replay is reported beside it).  The per-conv kernels (used by the
     # training path and the non-chained plan) are timed the same way on a single-stream,
     # full-batch, per-conv plan (under a split plan two half-batch launches share the CUs, so
     # a launch's duration is not its own).
@@ -376,7 +399,9 @@ def main():
     kernels = {}
     chained = (plan.subs[0] if n_streams > 1 else plan).chain is not None
     if chained and n_streams == 1:
-        c_ms, c_tags = time_family(plan, {("chain", 15 * args.blocks)}, stream, sp)
+        chain_tag = ("chain", 15 * args.blocks)
+        c_iso_ms, c_tags = time_family(plan, {chain_tag}, stream, sp)
+        c_ms, c_all = time_in_forward(plan, x, out, {chain_tag}, max(args.steps, 10))
         trunk_bytes = args.blocks * 3 * (sum(64 + 32 * k + 32 for k in range(4)) + 192 + 64) * 2 * npx
         trunk_flops = args.blocks * 3 * (sum(2.0 * 9 * (64 + 32 * k) * 32 for k in range(4))
                                          + 2.0 * 9 * 192 * 64) * npx
@@ -392,6 +417,9 @@ def main():
                             "frac": round(c_gbs / HBM_PEAK_GBS, 4), "traffic": traffic.get("chain"),
                             "bytes_per_launch": trunk_bytes, "flops_per_launch": trunk_flops,
                             "avg_launch_ms": round(c_ms, 5), "launches_per_step": len(c_tags),
+                            "timing": f"mean over {len(c_all)} launches inside back-to-back eager forwards "
+                                      "(bench.time_in_forward)",
+                            "avg_launch_ms_isolated": round(c_iso_ms, 5),
                             "lds_staged_bytes_per_launch": {"halo": staged_halo, "weights": staged_w,
                                                             "gb_s": round((staged_halo + staged_w) / (c_ms * 1e-3) / 1e9, 1)},
                             "mfma_frac": round(trunk_flops / (c_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
@@ -421,6 +449,9 @@ def main():
     # algorithmic bytes = its bf16 input once + the output once
     p0 = plan.subs[0] if n_streams > 1 else plan
     t_ms, t_tags = time_family(p0, {("tail9x9", 64, 3)}, stream, sp)
+    if n_streams == 1:  # in situ, as the trunk (the isolated replay stays beside it)
+        t_iso_ms = t_ms
+        t_ms, _ = time_in_forward(p0, x, out, {("tail9x9", 64, 3)}, max(args.steps, 10))
     hr_side = hw * S
     t_bytes = (n // max(1, n_streams)) * hr_side * hr_side * (64 * 2 + 3 * out.element_size())
     t_gbs = t_bytes / (t_ms * 1e-3) / 1e9
@@ -429,6 +460,7 @@ def main():
                        "achieved": round(t_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(t_gbs / HBM_PEAK_GBS, 4), "traffic": traffic.get("tail"),
                        "bytes_per_launch": t_bytes, "avg_launch_ms": round(t_ms, 5),
+                       **({"avg_launch_ms_isolated": round(t_iso_ms, 5)} if n_streams == 1 else {}),
                        "launches_per_step": len(t_tags) * max(1, n_streams),
                        "flops_per_launch": t_flops,
                        "mfma_frac": round(t_flops / (t_ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4)}
