@@ -20,9 +20,11 @@ graph (engine.GraphedPlan; --no-graph for the eager ctypes launch loop, whose
                   granularity bytes bind, B/BW > F/P).  Algorithmic bytes per launch
                   = 48 RDBs x (each conv's input read once + output written once:
                   832 channels) x 2 B x N*H*W = 20.9 GB at N=16, 128²; its launch is
-                  replayed back to back on the launch stream between one pair of HIP
-                  events (5 rounds, median), so the per-launch time matches
-                  rocprofv3's kernel trace of the same command.  traffic = PMC HBM
+                  timed INSIDE whole forwards run back to back (HIP events around the
+                  chain launch on its stream, time_in_forward), so the per-launch time
+                  matches rocprofv3's kernel trace of the same command (isolated
+                  launches after an idle gap run at a boosted clock: reported as
+                  avg_launch_ms_isolated, not used).  traffic = PMC HBM
                   bytes per launch from profiles/<round>_pmc_traffic.json
                   (rocprofv3 --pmc, corrected per MI355X_MICROARCH.md), or null.
   roofline_kernels — the chain kernel, the per-conv kernels it is built from, and the 9x9 tail
@@ -31,7 +33,7 @@ graph (engine.GraphedPlan; --no-graph for the eager ctypes launch loop, whose
                   2 B x N*H*W per launch) and the RDB final conv 192->64 (MFMA,
                   2*9*192*64 FLOP per output pixel), timed on a per-conv plan.
   model_roofline — SURVEY.md §8d: max(F / P_mfma, B / BW_hbm) / t_step for the
-                  whole forward (F = 410.9 GFLOP and B = 1.403 GB bf16 per 128²
+                  whole forward (F = 410.9 GFLOP and B = 1.403 GB of 2-byte storage per 128²
                   tile at layer granularity).
   cpu_baseline  — the parity-verified CPU restatement (oracle/ref_cpu.py, torch
                   fp32) on this host's CPUs available to the process (affinity,
