@@ -35,6 +35,9 @@ graph (engine.GraphedPlan; --no-graph for the eager ctypes launch loop, whose
   model_roofline — SURVEY.md §8d: max(F / P_mfma, B / BW_hbm) / t_step for the
                   whole forward (F = 410.9 GFLOP and B = 1.403 GB of 2-byte storage per 128²
                   tile at layer granularity).
+  storage_ab    — N=1 only: ms per step of the same forward with bf16 storage beside the fp16
+                  default, interleaved in this process (the ~4 % clock price of fp16, DESIGN.md
+                  round 6); informational, value is the fp16 default.
   cpu_baseline  — the parity-verified CPU restatement (oracle/ref_cpu.py, torch
                   fp32) on this host's CPUs available to the process (affinity,
                   capped by the cgroup CPU quota; the count is stated): the bench's
@@ -93,6 +96,8 @@ def parse():
                     help="tiles the CPU baseline runs one by one (the first is the warm-up; all of them are the "
                          "parity reference)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-storage-ab", dest="storage_ab", action="store_false",
+                    help="skip the informational bf16-vs-fp16 storage timing")
     ap.add_argument("--round", default="r06")  # PMC traffic file (profiles/<round>_pmc_traffic.json)
     ap.add_argument("--weights", default=str(ROOT / "tests" / "golden" / "trained_resnet_x4.safetensors"),
                     help="generator state_dict (default: the committed trained ResNet(16, 0.2, x4)); "
@@ -474,6 +479,32 @@ def main():
                       "mfma_frac": round(f_over_p / ms, 4), "hbm_frac": round(b_over_bw / ms, 4)}
 
     log("per-kernel roofline timings done")
+    # The storage trade of round 6 on this box: the same forward with bf16 storage
+    # (pack_generator(f16=False)), interleaved with the fp16 default in one process.  Informational:
+    # value / ms_per_step above are the fp16 default; bf16 misses the north-star bar at x2.
+    storage_ab = None
+    if world == 1 and n_streams == 1 and not args.no_graph and gw.dtype == torch.float16 and args.storage_ab:
+        gw_b = engine.pack_generator({k: v.to(dev) for k, v in sd_cpu.items()}, enchant=False, add_rate=0.2,
+                                     device=dev, f16=False)
+        plan_b = engine.GeneratorPlan(gw_b, n, hw, hw, dev, False, False, mean, std)
+        out_b = torch.empty_like(out)
+        run_b = engine.GraphedPlan(plan_b, x, out_b).run
+        reps, ts = max(5, args.steps // 2), {"fp16": [], "bf16": []}
+        for _ in range(3):
+            for name, fn in (("fp16", step), ("bf16", run_b)):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                torch.cuda.synchronize()
+                ts[name].append((time.perf_counter() - t1) / reps * 1e3)
+        plan_b.verify()
+        storage_ab = {k: round(statistics.median(v), 4) for k, v in ts.items()}
+        storage_ab.update({"unit": "ms_per_step", "rounds": 3, "steps_per_round": reps,
+                           "fp16_over_bf16": round(storage_ab["fp16"] / storage_ab["bf16"], 4)})
+        del plan_b, run_b, gw_b, out_b
+        torch.cuda.empty_cache()
+        log(f"storage A/B: fp16 {storage_ab['fp16']} ms, bf16 {storage_ab['bf16']} ms per step")
     train = train_leg(args, dev, world, rank) if args.train_steps > 0 else None
     if train is not None:
         log(f"train leg: {train['ms_per_step']} ms per step")
@@ -530,6 +561,7 @@ def main():
             "model_roofline": model_roofline,
             "model_tflops_per_s": round(model_flops / (ms * 1e-3) / 1e12, 2),
             "cpu_baseline": cpu,
+            "storage_ab": storage_ab,
             "parity": parity,
             "train": train,
         }

@@ -33,7 +33,7 @@ out = [{"kernel": k, "blocks": b, "dispatches": len(v), "avg_us": round(sum(v) /
 json.dump(out, open(sys.argv[2], "w"), indent=1)
 print(json.dumps(out))
 EOF2
-bash tools/profile_pmc.sh $T/pmc_bench bench.py --no-cpu-baseline --steps 5 --warmup 2 --train-steps 0 --round $R
+bash tools/profile_pmc.sh $T/pmc_bench bench.py --no-cpu-baseline --no-storage-ab --steps 5 --warmup 2 --train-steps 0 --round $R
 python3 tools/pmc_summary.py $T/pmc_bench --json $P/${R}_pmc_summary.json > /dev/null
 python3 - "$R" "$P" <<'EOF'
 import json, sys
