@@ -79,7 +79,9 @@ struct C3 {
     static constexpr int NA = R + TN - 1;  // input rows one wave reads per step
     static constexpr int CIN = CIN_; // 0 = runtime cin; else compile-time (own symbol)
     // Ablation bits, tuning builds only (outputs wrong): 1 = no MFMA (operands
-    // kept live), 2 = stage only chunk 0 (no refill), 4 = no epilogue stores.
+    // kept live), 2 = stage only chunk 0 (no refill), 4 = no epilogue stores, 8 = the weights of
+    // chunk 0 only (later chunks refill their halo but not their weights: the time a block would
+    // take with its weights resident in LDS, round 6 probe for the Scaler / VGG short-K convs).
     static constexpr int ABL = ABL_;
     static constexpr int TH = R * WM;
     static constexpr int TW = 32;
@@ -425,7 +427,7 @@ __device__ __forceinline__ void conv_tile(const Desc& d, int t, int srow = -1, c
             if (j < C::HALO_INSTR) {
                 if constexpr (HX) glds16_sc1(xs + o, dst + j * 1024);
                 else glds16(xs + o, dst + j * 1024);
-            } else {
+            } else if (!(C::ABL & 8) || chunk == 0) {
                 glds16(ws + o, dst + j * 1024);
             }
         }
@@ -808,6 +810,9 @@ int conv3x3_fwd_variant(const isr_conv_desc* d, int variant, hipStream_t s) {
                                      : launch3x3<C3<4, 4, 2, 16, 2, 0, 0, 2, 4, 1>>(d, s);
         case 9: return d->cin == 192 ? launch3x3<C3<4, 8, 2, 16, 2, 192, 0, 2>>(d, s)  // 32x32, 8 waves, PIPE 2 (111 KB)
                                      : launch3x3<C3<4, 8, 2, 16, 2, 0, 0, 2>>(d, s);
+        // timing probes (outputs wrong): V_W0 / variant 9 without the weight refills (ABL 8)
+        case 10: return launch3x3<C3<4, 4, 2, 16, 2, 0, 8, 2>>(d, s);
+        case 11: return launch3x3<C3<4, 8, 2, 16, 2, 0, 8, 2>>(d, s);
         // ablations of V_W0 (timing only, outputs wrong): tuning builds only
         case 4: return launch3x3<C3<4, 4, 2, 16, 2, 0, 1>>(d, s);
         case 5: return launch3x3<C3<4, 4, 2, 16, 2, 0, 2>>(d, s);
