@@ -9,7 +9,8 @@
  * INTEGRATION.md); no torch types cross this boundary.
  *
  * Conventions
- *  - Activations are channel-blocked bf16 ("NC16HW16c") in caller-owned device
+ *  - Activations are channel-blocked 2-byte floats ("NC16HW16c": bf16, or fp16 on the
+ *    forward descriptors with f16 = 1, the inference default since round 6) in caller-owned device
  *    buffers laid out as [N][cs/16][hp][wp][16] with a zero border of `pad`
  *    pixels on every side: each 16-channel block is a contiguous plane, so a
  *    K-chunk of a convolution reads whole cache lines.  The caller zero-fills a
@@ -42,7 +43,7 @@ typedef struct ihipStream_t* isr_stream_t; /* == hipStream_t */
 #define ISR_TILE_H 32
 #define ISR_TILE_W 32
 
-/* A channel slice [coff, coff + k) of a channel-blocked bf16 buffer
+/* A channel slice [coff, coff + k) of a channel-blocked bf16 / fp16 buffer
  * [N][cs/16][hp][wp][16] with border `pad` (cs, coff multiples of 16).
  * Interior pixel (n, y, x), view channel c (ch = coff + c) lives at
  *   data + ((((n*(cs/16) + ch/16)*hp + y + pad)*wp + x + pad)*16 + ch%16) * 2 bytes. */
