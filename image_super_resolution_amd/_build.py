@@ -151,6 +151,26 @@ def build_probe16(verbose: bool = False) -> Path:
     return lib_path
 
 
+def build_trunk_alt(tag: str, defines: list[str], verbose: bool = False) -> Path:
+    """lib/libisr_<tag>.so: the production objects with trunk.hip rebuilt under `defines` (A/B of a
+    production trunk option in alternating processes, e.g. tag "xcd", ["-DISR_TRUNK_XCD=1"])."""
+    build(verbose=verbose)
+    objdir = PKG / f"build_{tag}"
+    objdir.mkdir(exist_ok=True)
+    trunk_obj = objdir / "trunk.o"
+    r = subprocess.run([HIPCC, *FLAGS, *defines, "-c", str(CSRC / "trunk.hip"), "-o", str(trunk_obj)],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed on trunk.hip ({tag}):\n{r.stderr}")
+    objs = [trunk_obj if src.stem == "trunk" else PKG / "build" / (src.stem + ".o") for src in sources()]
+    lib_path = LIBDIR / f"libisr_{tag}.so"
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib_path), *map(str, objs)],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return lib_path
+
+
 if __name__ == "__main__":
     if "--probe16" in sys.argv:
         print(build_probe16(verbose=True))

@@ -1022,7 +1022,12 @@ static int trunk_launch_k(const isr_chain_desc* cd, hipStream_t s) {
 // the RRDB residual is loaded row by row in the epilogue): 6.46 ms per bench forward against
 // 7.77 ms for the deep form (same box, tools/ab_chain.py, profiles/r03_ab_chain.jsonl) — the deep
 // form's 2-row waves read 7 LDS fragments per 6 MFMAs (4-row waves: 9 per 12)
-using TK_PAIR = TK<4, 4, 2>;
+// ISR_TRUNK_XCD=1 (A/B build lib/libisr_xcd.so, _build.build_trunk_alt): the same form with the
+// XCD-aware tile deal (each XCD streams a contiguous range of tiles; bit-identical outputs)
+#ifndef ISR_TRUNK_XCD
+#define ISR_TRUNK_XCD 0
+#endif
+using TK_PAIR = TK<4, 4, 2, 16, ISR_TRUNK_XCD>;
 
 // The A/B forms below measured slower than the pair form on the same boxes and are
 // compiled only into the tuning library (-DISR_TUNING, lib/libisr_tuning.so): the production
