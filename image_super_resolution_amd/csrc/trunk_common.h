@@ -65,6 +65,13 @@ __device__ __forceinline__ int nb_of(int t, int nbx, int nby) {
     return (yy >= 0 && yy < nby && xx >= 0 && xx < nbx) ? (img * nby + yy) * nbx + xx : -1;
 }
 
+// s_sleep between two polls of a dependency wait (units of 64 clocks).  A spinning wave's polls
+// take issue slots from the wave computing beside it on the same SIMD (the other workgroup of the
+// CU) and draw power under the clock cap; A/B builds: _build.build_trunk_alt.
+#ifndef ISR_TRUNK_SPIN_SLEEP
+#define ISR_TRUNK_SPIN_SLEEP 1
+#endif
+
 __device__ __forceinline__ unsigned poll_load(const unsigned* progress, int nb) {
     return __hip_atomic_load(progress + (nb < 0 ? 0 : nb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -86,7 +93,7 @@ __device__ __forceinline__ void dep_wait(unsigned* state, int nb, unsigned need,
             }
             break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(ISR_TRUNK_SPIN_SLEEP);
     }
 }
 
